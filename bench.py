@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""bench.py -- GDM operator application (vmult) throughput on MI355X.
+
+Metric (BASELINE.json): DoF-updates/s of the 3D advection GDM stiffness action
+(StiffnessMatrixOperator::compute_rhs, applications/advection/include/gdm/
+advection/stiffness.h:196-606, uncut, alpha = 0) at p = 5 on 512^3 DoFs per
+GPU, plus achieved HBM GB/s of the dominant kernel against the 8 TB/s roofline.
+
+One step = ghost-plane exchange (N > 1) + fused Kronecker stencil kernel
+(volume term + outflow traces) + inflow boundary-data kernels, on inputs that
+are resident in HBM.  Weak scaling: each rank owns one 512-plane z-slab of a
+512 x 512 x 512N vertex grid partitioned with the reference's slab formula
+(system.h:720-757); --strong keeps the global grid at 512^3 instead.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dealii-galerkin-difference-methods_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+BYTES_PER_DOF = 16.0   # algorithmic: read u once + write v once, fp64
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=511, help="cells per direction per GPU slab (vertices = n + 1)")
+    ap.add_argument("--p", type=int, default=5)
+    ap.add_argument("--kind", default="advection", choices=["advection", "wave", "mass"])
+    ap.add_argument("--strong", action="store_true", help="fixed global grid instead of one slab per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-cells", type=int, default=24, help="cells per direction of the CPU-baseline sample")
+    ap.add_argument("--pmc", default=os.environ.get("GDM_BENCH_PMC", "1"), help="collect HBM PMC traffic (1/0)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+def cpu_baseline(p, n_cells):
+    """Reference algorithm (per-cell FEValues loop of stiffness.h:345-532) from
+    the CPU restatement in oracle/, single thread, on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    m = O.Mesh(3, p, n_cells, 0.0, 1.0)
+    u = np.random.default_rng(20251010).uniform(-1, 1, m.n_dofs)
+    bc = np.random.default_rng(1).uniform(-1, 1, m.n_boundary_points())
+    a = (1.0, 0.15, -0.05)
+    O.Mesh(3, p, p + 1).advection_rhs(a, np.zeros((p + 2) ** 3), None)  # load the library
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        m.advection_rhs(a, u, bc)
+        reps += 1
+        if time.perf_counter() - t0 > 10.0:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    return {
+        "value": m.n_dofs / dt,
+        "unit": "DoF-updates/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "3D p=%d advection compute_rhs, reference per-cell algorithm (oracle/gdm_oracle.c), "
+                  "%d^3 cells = %d DoFs, %d application(s) in %.1f s, 1 thread" % (p, n_cells, m.n_dofs, reps, dt * reps),
+    }
+
+
+def pmc_traffic(args):
+    """HBM bytes per stencil launch from rocprofv3 PMC counters, collected in
+    separate passes (FETCH_SIZE, WRITE_SIZE) by a child process; FETCH_SIZE is
+    doubled per MI355X_MICROARCH.md 'HBM' (gfx950 reports half of a wide
+    coalesced stream).  Returns bytes or None."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+
+    if not shutil.which("rocprofv3"):
+        return None
+    res = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = tempfile.mkdtemp(prefix="gdm_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = ["rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--n", str(args.n), "--p", str(args.p),
+               "--kind", args.kind]
+        try:
+            subprocess.run(cmd, check=True, timeout=300, capture_output=True, cwd=ROOT)
+        except Exception:
+            return None
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        vals = []
+        for f in files:
+            for row in csv.DictReader(open(f)):
+                if "stencil3d_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    vals.append(float(row["Counter_Value"]))
+        shutil.rmtree(out, ignore_errors=True)
+        if not vals:
+            return None
+        res[ctr] = sorted(vals)[len(vals) // 2]  # median over launches, KiB
+    return (2.0 * res["FETCH_SIZE"] + res["WRITE_SIZE"]) * 1024.0
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from gdm_amd import GdmOperator
+    from gdm_amd.distributed import HaloExchange
+
+    p, n = args.p, args.n
+    nz_cells = n if (args.strong or world == 1) else (n + 1) * world - 1
+    n_sub = (n, n, nz_cells)
+    hi = (1.0, 1.0, nz_cells / n)  # uniform h = 1/n
+    a = (1.0, 0.15, -0.05)        # advection_01_gdm.cc:37-41
+    params = a if args.kind == "advection" else ()
+    op = GdmOperator(3, p, n_sub, (0.0, 0.0, 0.0), hi, args.kind, params=params, rank=rank, n_ranks=world,
+                     device=local_rank)
+    lay = op.layout
+    gen = torch.Generator(device="cuda").manual_seed(20251010 + rank)
+    src = torch.rand(op.n_local, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+    dst = op.new_vector(local=False)
+    bc = None
+    if args.kind == "advection" and op.n_bc_points > 0:
+        bc = torch.rand(op.n_bc_points, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+
+    if args.pmc_child:
+        for _ in range(3):
+            op.apply(src, dst)
+        torch.cuda.synchronize()
+        return
+
+    halo = HaloExchange(nz_cells, world, rank, lay["plane_size"], lay["halo_depth"]) if world > 1 else None
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if halo is not None:
+            halo.exchange(src)
+        if ev is not None:
+            ev[0].record(stream)
+        op.apply(src, dst)
+        if ev is not None:
+            ev[1].record(stream)
+        if bc is not None:
+            op.add_boundary_data(bc, dst)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / args.steps
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    total_dofs = lay["n_dofs_global"]
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_dofs * args.steps / elapsed
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    achieved = BYTES_PER_DOF * lay["n_owned"] / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if world == 1 and str(args.pmc) == "1":
+        traffic = pmc_traffic(args)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(p, args.cpu_cells)
+        except Exception as e:  # the baseline never blocks the GPU line
+            cpu = {"value": None, "error": str(e)}
+    out = {
+        "metric": "DoF-updates/sec (vmult) + achieved HBM GB/s, 3D advection p=5 at 1/2/4/8 GPUs",
+        "value": value,
+        "unit": "DoF-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong" if args.strong else "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: u ~ U[-1,1) seeded, stage boundary values ~ U[-1,1); inputs resident in HBM",
+        "config": {
+            "workload": "3D %s GDM compute_rhs (uncut), p=%d, %dx%dx%d vertices global, %d vertex planes per rank"
+                        % (args.kind, p, n + 1, n + 1, nz_cells + 1, lay["owned_plane_end"] - lay["owned_plane_begin"]),
+            "fe_degree": p,
+            "n_dofs_global": total_dofs,
+            "n_dofs_per_gpu": lay["n_owned"],
+            "advection": list(a) if args.kind == "advection" else None,
+            "partition": "z-slabs, system.h:720-757 formula, %d ghost planes per side" % lay["halo_depth"],
+            "parallelism": "slab%d" % world,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "stencil3d_kernel<%d> (fused Kronecker stencil)" % p,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel_ms": kern_ms,
+            "algorithmic_bytes_per_launch": BYTES_PER_DOF * lay["n_owned"],
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,728 @@
+// gdm_capi.cpp -- C ABI of libgdm_hip.so (declared in include/gdm_hip.h).
+//
+// Owns the device-side operator state: 1D band tables in kernel order, the
+// banded Cholesky factors of the 1D mass matrices, the inflow-face projection
+// tables and the slab layout.  All launches go to the operator's stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/gdm_hip.h"
+#include "gdm_kernels.h"
+#include "gdm_setup.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char *what) {
+  if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename T>
+T *dev_upload(const std::vector<T> &h) {
+  T *d = nullptr;
+  const size_t bytes = std::max<size_t>(h.size(), 1) * sizeof(T);
+  hip_check(hipMalloc(&d, bytes), "hipMalloc");
+  if (!h.empty()) hip_check(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
+  return d;
+}
+
+// one tangential direction of a boundary face
+struct FaceDir {
+  int dim_index = -1;     // reference direction, -1 = trivial
+  int n_nodes = 1;        // nodes along this direction
+  int Q = 1;              // quadrature points along this direction (local cells x (p+1))
+  int cell_begin = 0;     // first local cell
+  int node_begin = 0, node_end = 1;  // output node range (owned)
+  int64_t stride = 0;     // global index stride
+  int wmax = 1;
+  int *qs = nullptr, *qc = nullptr;
+  double *w = nullptr;
+};
+
+struct Face {
+  int d = 0, side = 0;
+  double scale = 0.0;     // |a.n| for inflow faces, 0 otherwise
+  int64_t offset = 0;     // offset into the device bc array
+  int64_t n_points = 0;
+  FaceDir t0, t1;
+  int64_t base = 0;       // owned index of node (i0 = 0, i1 = t1.node_begin)
+};
+
+}  // namespace
+
+struct gdm_op {
+  int device = 0;
+  hipStream_t own_stream = nullptr, stream = nullptr;
+  gdm_mesh_desc mesh{};
+  int kind = 0, p = 1, dim = 1;
+  int N[3] = {1, 1, 1};        // vertices per reference direction
+  int K[3] = {1, 1, 1};        // kernel-space extents (X, Y, Z)
+  int kdir[3] = {-1, -1, -1};  // kernel axis -> reference direction (-1 trivial)
+  int part_axis = 2;           // kernel axis of the slab partition (1 = Y, 2 = Z)
+  gdm_layout layout{};
+  double a[3] = {0, 0, 0};
+  double nitsche = 0.0;
+  // device tables
+  double *rowMx = nullptr, *rowBx = nullptr, *colMy = nullptr, *colBy = nullptr, *colMz = nullptr, *colBz = nullptr;
+  double *lrow[3] = {nullptr, nullptr, nullptr}, *invd[3] = {nullptr, nullptr, nullptr};
+  std::vector<Face> faces;
+  double *face_tmp = nullptr;
+  int64_t face_tmp_size = 0;
+  double *dot_partial = nullptr, *dot_out = nullptr;
+  int n_dot_partial = 1024;
+  int zchunk = 64;
+  // host copies for bc ordering
+  std::vector<double> xq;
+  gdm::Slab slab{};
+  std::vector<void *> allocations;
+};
+
+namespace {
+
+void free_op(gdm_op *op) {
+  if (!op) return;
+  for (void *ptr : op->allocations) (void)hipFree(ptr);
+  if (op->own_stream) (void)hipStreamDestroy(op->own_stream);
+  delete op;
+}
+
+template <typename T>
+T *keep(gdm_op *op, T *ptr) {
+  op->allocations.push_back((void *)ptr);
+  return ptr;
+}
+
+// Build the row (x) or column (y, z) band table of a kernel axis in kernel
+// order.  For column tables entry [s][k] holds A(s - p + k, s).
+std::vector<double> band_rows(const gdm::Band &A) { return A.a; }
+
+std::vector<double> band_cols(const gdm::Band &A, int pad, int pad_back) {
+  // rows [0, pad) and [pad + n, pad + n + pad_back) are zero: the kernel reads
+  // them for halo rows outside the domain and for rows of a partial last tile
+  const int n = A.n, hb = A.hb, W = 2 * hb + 1;
+  std::vector<double> t((size_t)(n + pad + pad_back) * W, 0.0);
+  for (int s = 0; s < n; ++s)
+    for (int k = 0; k < W; ++k) t[(size_t)(s + pad) * W + k] = A(s - hb + k, s);
+  return t;
+}
+
+gdm::Band identity_band(int p) {
+  gdm::Band b(1, p);
+  b(0, 0) = 1.0;
+  return b;
+}
+
+void build_tables(gdm_op *op) {
+  const int p = op->p;
+  gdm::Band M[3], B[3];
+  for (int ax = 0; ax < 3; ++ax) {
+    const int d = op->kdir[ax];
+    if (d < 0) {
+      M[ax] = identity_band(p);
+      B[ax] = gdm::Band(1, p);
+      continue;
+    }
+    const unsigned ncell = (unsigned)op->mesh.n_subdivisions[d];
+    const double h = (op->mesh.hi[d] - op->mesh.lo[d]) / ncell;
+    gdm::Matrices1D m = gdm::assemble_1d(p, ncell, h);
+    M[ax] = m.M;
+    const int n = m.M.n, last = n - 1;
+    gdm::Band b(n, p);
+    switch (op->kind) {
+      case GDM_OP_ADVECTION: {
+        // (a u, grad v): a_d C_d; outflow faces (a.n >= 0) add -(a.n) u v
+        // (stiffness.h:411-417, :520-529)
+        const double ad = op->a[d];
+        for (int i = 0; i < n; ++i)
+          for (int j = std::max(0, i - p); j <= std::min(last, i + p); ++j) b(i, j) = ad * m.C(i, j);
+        if (ad >= 0.0) b(last, last) -= ad;    // right face, a.n = a_d
+        if (-ad >= 0.0) b(0, 0) += ad;         // left face, a.n = -a_d
+        break;
+      }
+      case GDM_OP_CONVECTIVE: {
+        // -(a . grad u, v): -a_d C^T (advection_01_gdm.cc:199-203)
+        const double ad = op->a[d];
+        for (int i = 0; i < n; ++i)
+          for (int j = std::max(0, i - p); j <= std::min(last, i + p); ++j) b(i, j) = -ad * m.C(j, i);
+        break;
+      }
+      case GDM_OP_WAVE: {
+        // -(grad v, grad u) (wave/stiffness.h:171-181) + box Nitsche
+        // (:296-310): -[-dv/dn u - v du/dn + gamma/h v u] on each box face
+        for (int i = 0; i < n; ++i)
+          for (int j = std::max(0, i - p); j <= std::min(last, i + p); ++j) b(i, j) = -m.L(i, j);
+        if (op->nitsche > 0.0) {
+          double hmin = 1e300;
+          for (int e = 0; e < op->dim; ++e)
+            hmin = std::min(hmin, (op->mesh.hi[e] - op->mesh.lo[e]) / op->mesh.n_subdivisions[e]);
+          // traces of the boundary cells
+          const unsigned cl = 0, cr = ncell - 1;
+          const int catl = (int)gdm::category(cl, p, ncell), catr = (int)gdm::category(cr, p, ncell);
+          const int offl = (int)gdm::box_offset(cl, p, ncell), offr = (int)gdm::box_offset(cr, p, ncell);
+          for (int side = 0; side < 2; ++side) {
+            const int cat = side ? catr : catl, off = side ? offr : offl;
+            const double x = side ? 1.0 : 0.0, nrm = side ? 1.0 : -1.0;
+            for (int ii = 0; ii <= p; ++ii)
+              for (int jj = 0; jj <= p; ++jj) {
+                const double vi = gdm::shape_1d(p, cat, ii, x, 0), vj = gdm::shape_1d(p, cat, jj, x, 0);
+                const double di = gdm::shape_1d(p, cat, ii, x, 1) / h * nrm;
+                const double dj = gdm::shape_1d(p, cat, jj, x, 1) / h * nrm;
+                b(off + ii, off + jj) -= (-di * vj - vi * dj + op->nitsche / hmin * vi * vj);
+              }
+          }
+        }
+        break;
+      }
+      default:
+        break;  // mass: B unused
+    }
+    B[ax] = b;
+  }
+  op->rowMx = keep(op, dev_upload(band_rows(M[0])));
+  op->rowBx = keep(op, dev_upload(band_rows(B[0])));
+  const int ypad = p + 64;  // >= p + max tile rows
+  op->colMy = keep(op, dev_upload(band_cols(M[1], p, ypad)));
+  op->colBy = keep(op, dev_upload(band_cols(B[1], p, ypad)));
+  op->colMz = keep(op, dev_upload(band_cols(M[2], 0, 0)));
+  op->colBz = keep(op, dev_upload(band_cols(B[2], 0, 0)));
+  // banded Cholesky factors of the 1D mass matrices (exact Kronecker inverse)
+  for (int ax = 0; ax < 3; ++ax) {
+    if (op->K[ax] <= 1) continue;
+    std::vector<double> lrow, invd;
+    gdm::cholesky_band(M[ax], lrow, invd);
+    lrow.resize(lrow.size() + (size_t)p * (p + 1), 0.0);  // zero pad for the backward sweep
+    op->lrow[ax] = keep(op, dev_upload(lrow));
+    op->invd[ax] = keep(op, dev_upload(invd));
+  }
+}
+
+void build_layout(gdm_op *op) {
+  const int q = op->dim - 1;  // partition direction (reference)
+  const unsigned ncq = (unsigned)op->mesh.n_subdivisions[q];
+  op->slab = gdm::slab_partition(ncq, (unsigned)op->mesh.n_ranks, (unsigned)op->mesh.rank);
+  gdm_layout &L = op->layout;
+  L.n_dofs_global = (int64_t)op->N[0] * op->N[1] * op->N[2];
+  L.plane_size = L.n_dofs_global / op->N[q];
+  L.n_planes_global = op->N[q];
+  L.owned_plane_begin = (int32_t)op->slab.plane_begin;
+  L.owned_plane_end = (int32_t)std::max(op->slab.plane_begin, op->slab.plane_end);
+  L.cell_plane_begin = (int32_t)op->slab.cell_begin;
+  L.cell_plane_end = (int32_t)std::max(op->slab.cell_begin, op->slab.cell_end);
+  L.halo_depth = op->p;
+  const int nown = L.owned_plane_end - L.owned_plane_begin;
+  if (nown > 0) {
+    L.ghost_planes_below = std::min(op->p, L.owned_plane_begin);
+    L.ghost_planes_above = std::min(op->p, op->N[q] - L.owned_plane_end);
+  } else {
+    L.ghost_planes_below = L.ghost_planes_above = 0;
+  }
+  L.n_owned = (int64_t)nown * L.plane_size;
+  L.n_local = (int64_t)(nown + L.ghost_planes_below + L.ghost_planes_above) * L.plane_size;
+}
+
+void build_faces(gdm_op *op) {
+  const int p = op->p, n1 = p + 1, dim = op->dim, q = dim - 1;
+  const gdm_layout &L = op->layout;
+  int64_t stride[3] = {1, op->N[0], (int64_t)op->N[0] * op->N[1]};
+  const int64_t own_off = (int64_t)L.owned_plane_begin * L.plane_size;
+  int64_t offset = 0;
+  int64_t max_tmp = 1;
+  const bool have_cells = L.cell_plane_end > L.cell_plane_begin;
+  for (int f = 0; f < 2 * dim && have_cells; ++f) {
+    const int d = f / 2, side = f % 2;
+    const unsigned ncd = (unsigned)op->mesh.n_subdivisions[d];
+    // does this rank own cells adjacent to the face?
+    if (d == q) {
+      if (side == 0 && L.cell_plane_begin != 0) continue;
+      if (side == 1 && L.cell_plane_end != (int)ncd) continue;
+    }
+    Face F;
+    F.d = d;
+    F.side = side;
+    const double an = side ? op->a[d] : -op->a[d];
+    F.scale = (op->kind == GDM_OP_ADVECTION && an < 0.0) ? -an : 0.0;
+    int tang[2] = {-1, -1}, nt = 0;
+    for (int e = 0; e < dim; ++e)
+      if (e != d) tang[nt++] = e;
+    FaceDir *T[2] = {&F.t0, &F.t1};
+    for (int k = 0; k < 2; ++k) {
+      FaceDir &t = *T[k];
+      const int e = tang[k];
+      t.dim_index = e;
+      if (e < 0) {
+        std::vector<int32_t> qs{0}, qc{1};
+        std::vector<double> w{1.0};
+        t.n_nodes = 1;
+        t.Q = 1;
+        t.node_begin = 0;
+        t.node_end = 1;
+        t.stride = 0;
+        t.wmax = 1;
+        t.qs = keep(op, dev_upload(qs));
+        t.qc = keep(op, dev_upload(qc));
+        t.w = keep(op, dev_upload(w));
+        continue;
+      }
+      const unsigned nce = (unsigned)op->mesh.n_subdivisions[e];
+      const double h = (op->mesh.hi[e] - op->mesh.lo[e]) / nce;
+      unsigned cb = 0, ce = nce;
+      int nb = 0, ne = op->N[e];
+      if (e == q) {
+        cb = (unsigned)L.cell_plane_begin;
+        ce = (unsigned)L.cell_plane_end;
+        nb = L.owned_plane_begin;
+        ne = L.owned_plane_end;
+      }
+      gdm::FaceTable ft = gdm::face_table_1d(p, nce, h, cb, ce);
+      t.n_nodes = op->N[e];
+      t.Q = int(ce - cb) * n1;
+      t.cell_begin = (int)cb;
+      t.node_begin = nb;
+      t.node_end = ne;
+      t.stride = stride[e];
+      t.wmax = ft.wmax;
+      t.qs = keep(op, dev_upload(ft.qstart));
+      t.qc = keep(op, dev_upload(ft.qcount));
+      t.w = keep(op, dev_upload(ft.w));
+    }
+    F.n_points = (int64_t)F.t0.Q * F.t1.Q;
+    F.offset = offset;
+    offset += F.n_points;
+    const int64_t node_d = side ? (op->N[d] - 1) : 0;
+    F.base = node_d * stride[d] + (int64_t)F.t0.node_begin * F.t0.stride + (int64_t)F.t1.node_begin * F.t1.stride -
+             own_off;
+    max_tmp = std::max<int64_t>(max_tmp, (int64_t)F.t1.Q * (F.t0.node_end - F.t0.node_begin));
+    op->faces.push_back(F);
+  }
+  op->layout.n_bc_points = offset;
+  op->face_tmp_size = max_tmp;
+  hip_check(hipMalloc(&op->face_tmp, sizeof(double) * max_tmp), "hipMalloc");
+  keep(op, op->face_tmp);
+}
+
+hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst) {
+  const gdm_layout &L = op->layout;
+  gdmk::StencilArgs a{};
+  a.src = src;
+  a.dst = dst;
+  a.Nx = op->K[0];
+  a.Ny = op->K[1];
+  a.Nz = op->K[2];
+  const int ib = L.owned_plane_begin - L.ghost_planes_below, ie = L.owned_plane_end + L.ghost_planes_above;
+  if (op->part_axis == 2) {
+    a.in_y0 = 0; a.in_y1 = a.Ny; a.in_z0 = ib; a.in_z1 = ie;
+    a.out_y0 = 0; a.out_y1 = a.Ny; a.out_z0 = L.owned_plane_begin; a.out_z1 = L.owned_plane_end;
+  } else {
+    a.in_z0 = 0; a.in_z1 = 1; a.in_y0 = ib; a.in_y1 = ie;
+    a.out_z0 = 0; a.out_z1 = 1; a.out_y0 = L.owned_plane_begin; a.out_y1 = L.owned_plane_end;
+  }
+  a.zchunk = std::max(1, std::min(op->zchunk, a.out_z1 - a.out_z0));
+  a.rowMx = op->rowMx;
+  a.rowBx = op->rowBx;
+  a.colMy = op->colMy;
+  a.colBy = op->colBy;
+  a.colMz = op->colMz;
+  a.colBz = op->colBz;
+  if (L.n_owned == 0) return hipSuccess;
+  return gdmk_launch_stencil(op->p, mass, a, op->stream);
+}
+
+void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned) {
+  if (op->kind != GDM_OP_ADVECTION) return;
+  {
+    for (const Face &F : op->faces) {
+      if (F.scale == 0.0) continue;
+      gdmk::FaceArgs fa{};
+      fa.U = bc_values + F.offset;
+      fa.Q0 = F.t0.Q;
+      fa.Q1 = F.t1.Q;
+      fa.i0_begin = F.t0.node_begin;
+      fa.i0_end = F.t0.node_end;
+      fa.i1_begin = F.t1.node_begin;
+      fa.i1_end = F.t1.node_end;
+      fa.qs0 = F.t0.qs;
+      fa.qc0 = F.t0.qc;
+      fa.w0 = F.t0.w;
+      fa.wmax0 = F.t0.wmax;
+      fa.qs1 = F.t1.qs;
+      fa.qc1 = F.t1.qc;
+      fa.w1 = F.t1.w;
+      fa.wmax1 = F.t1.wmax;
+      fa.T = op->face_tmp;
+      fa.dst = dst_owned;
+      fa.base = F.base;
+      fa.stride0 = F.t0.stride;
+      fa.stride1 = F.t1.stride;
+      fa.scale = F.scale;
+      hip_check(gdmk_launch_face(fa, op->stream), "face launch");
+    }
+  }
+}
+
+int choose_zchunk(const gdm_op *op) {
+  if (const char *env = std::getenv("GDM_ZCHUNK")) return std::max(1, std::atoi(env));
+  const int nz = op->part_axis == 2 ? (op->layout.owned_plane_end - op->layout.owned_plane_begin) : 1;
+  const int ty = gdmk_stencil_tile_rows(op->p);
+  const int64_t tiles = (int64_t)((op->K[0] + 63) / 64) * ((op->K[1] + ty - 1) / ty);
+  // aim for ~512 workgroups (2 rounds of one 8-wave workgroup per CU)
+  const int64_t chunks = std::max<int64_t>(1, (512 + tiles - 1) / tiles);
+  int zc = (int)std::max<int64_t>(8, (nz + chunks - 1) / chunks);
+  return std::max(1, zc);
+}
+
+#define GDM_GUARD_BEGIN try {
+#define GDM_GUARD_END                                             \
+  }                                                               \
+  catch (const HipError &e) { return fail(GDM_ERR_HIP, e.what()); } \
+  catch (const std::bad_alloc &) { return fail(GDM_ERR_NOMEM, "out of host memory"); } \
+  catch (const std::invalid_argument &e) { return fail(GDM_ERR_ARG, e.what()); } \
+  catch (const std::exception &e) { return fail(GDM_ERR_STATE, e.what()); }
+
+}  // namespace
+
+extern "C" {
+
+int gdm_last_error(char *buf, size_t len) {
+  if (!buf || len == 0) return GDM_ERR_ARG;
+  std::snprintf(buf, len, "%s", g_last_error.c_str());
+  return GDM_OK;
+}
+
+int gdm_abi_version(void) { return GDM_HIP_ABI_VERSION; }
+
+int gdm_get_device_count(int *n) {
+  if (!n) return fail(GDM_ERR_ARG, "n is NULL");
+  hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess) {
+    *n = 0;
+    return fail(GDM_ERR_HIP, hipGetErrorString(e));
+  }
+  return GDM_OK;
+}
+
+int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int n_params, int device,
+                  gdm_op **out) {
+  if (!mesh || !out) return fail(GDM_ERR_ARG, "mesh/out is NULL");
+  *out = nullptr;
+  const int dim = mesh->dim, p = mesh->fe_degree;
+  if (dim < 1 || dim > 3) return fail(GDM_ERR_ARG, "dim must be 1, 2 or 3");
+  if (p < 1 || p > 9 || p % 2 == 0)
+    return fail(GDM_ERR_UNSUPPORTED, "fe_degree must be odd in [1, 9] (fe.h:321-323 tabulates odd p only)");
+  if (kind < GDM_OP_MASS || kind > GDM_OP_CONVECTIVE) return fail(GDM_ERR_ARG, "unknown operator kind");
+  for (int d = 0; d < dim; ++d) {
+    if (mesh->n_subdivisions[d] < p)
+      return fail(GDM_ERR_ARG, "n_subdivisions must be >= fe_degree in every direction");
+    if (!(mesh->hi[d] > mesh->lo[d])) return fail(GDM_ERR_ARG, "empty box");
+  }
+  if (mesh->n_ranks < 1 || mesh->rank < 0 || mesh->rank >= mesh->n_ranks) return fail(GDM_ERR_ARG, "bad rank");
+  if (mesh->periodic != 0) return fail(GDM_ERR_UNSUPPORTED, "periodic constraints are not supported by the device path yet");
+  if ((kind == GDM_OP_ADVECTION || kind == GDM_OP_CONVECTIVE) && (n_params < dim || !params))
+    return fail(GDM_ERR_ARG, "advection needs the constant field a (dim values)");
+  gdm_op *op = new (std::nothrow) gdm_op();
+  if (!op) return fail(GDM_ERR_NOMEM, "out of host memory");
+  GDM_GUARD_BEGIN
+  op->device = device;
+  op->mesh = *mesh;
+  op->kind = kind;
+  op->p = p;
+  op->dim = dim;
+  for (int d = 0; d < dim; ++d) op->N[d] = mesh->n_subdivisions[d] + 1;
+  if (kind == GDM_OP_ADVECTION || kind == GDM_OP_CONVECTIVE)
+    for (int d = 0; d < dim; ++d) op->a[d] = params[d];
+  if (kind == GDM_OP_WAVE && n_params >= 1 && params) op->nitsche = params[0];
+  // kernel axes: 3D (x, y, z) partition z; 2D (x, y, -) partition y; 1D (-, -, x) partition z
+  if (dim == 3) {
+    op->kdir[0] = 0; op->kdir[1] = 1; op->kdir[2] = 2; op->part_axis = 2;
+  } else if (dim == 2) {
+    op->kdir[0] = 0; op->kdir[1] = 1; op->kdir[2] = -1; op->part_axis = 1;
+  } else {
+    op->kdir[0] = -1; op->kdir[1] = -1; op->kdir[2] = 0; op->part_axis = 2;
+  }
+  for (int ax = 0; ax < 3; ++ax) op->K[ax] = op->kdir[ax] < 0 ? 1 : op->N[op->kdir[ax]];
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  hip_check(hipStreamCreateWithFlags(&op->own_stream, hipStreamNonBlocking), "hipStreamCreate");
+  op->stream = op->own_stream;
+  build_layout(op);
+  build_tables(op);
+  build_faces(op);
+  op->zchunk = choose_zchunk(op);
+  hip_check(hipMalloc(&op->dot_partial, sizeof(double) * op->n_dot_partial), "hipMalloc");
+  keep(op, op->dot_partial);
+  hip_check(hipMalloc(&op->dot_out, sizeof(double)), "hipMalloc");
+  keep(op, op->dot_out);
+  {
+    std::vector<double> w;
+    gdm::gauss_unit(p + 1, op->xq, w);
+  }
+  *out = op;
+  return GDM_OK;
+  }
+  catch (const HipError &e) { free_op(op); return fail(GDM_ERR_HIP, e.what()); }
+  catch (const std::bad_alloc &) { free_op(op); return fail(GDM_ERR_NOMEM, "out of host memory"); }
+  catch (const std::invalid_argument &e) { free_op(op); return fail(GDM_ERR_ARG, e.what()); }
+  catch (const std::exception &e) { free_op(op); return fail(GDM_ERR_STATE, e.what()); }
+}
+
+int gdm_op_destroy(gdm_op *op) {
+  if (!op) return GDM_OK;
+  (void)hipSetDevice(op->device);
+  if (op->own_stream) (void)hipStreamSynchronize(op->own_stream);
+  free_op(op);
+  return GDM_OK;
+}
+
+int gdm_op_layout(const gdm_op *op, gdm_layout *out) {
+  if (!op || !out) return fail(GDM_ERR_ARG, "op/out is NULL");
+  *out = op->layout;
+  return GDM_OK;
+}
+
+int gdm_op_set_stream(gdm_op *op, void *hip_stream) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  op->stream = (hipStream_t)hip_stream;
+  return GDM_OK;
+}
+
+int gdm_op_use_own_stream(gdm_op *op) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  op->stream = op->own_stream;
+  return GDM_OK;
+}
+
+int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const double *bc_values) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned), "stencil launch");
+  if (bc_values) launch_boundary_data(op, bc_values, dst_owned);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_add_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_bc_points > 0 && (!bc_values || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  launch_boundary_data(op, bc_values, dst_owned);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_mass_apply(gdm_op *op, const double *src_local, double *dst_owned) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  hip_check(launch_stencil(op, true, src_local, dst_owned), "stencil launch");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->mesh.n_ranks != 1)
+    return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve: the exact Kronecker inverse is single-rank in this version");
+  if (!rhs_owned || !x_owned) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  const int64_t n = op->layout.n_owned;
+  if (x_owned != rhs_owned)
+    hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+  const int64_t X = op->K[0], Y = op->K[1], Z = op->K[2];
+  // z lines: (x, y) -> base = l, stride X*Y
+  if (Z > 1)
+    hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)Z, X * Y, X * Y, X * Y, 0, 1, op->lrow[2], op->invd[2],
+                                     op->stream), "chol z");
+  // y lines: (x, z) -> base = z*X*Y + x, stride X
+  if (Y > 1)
+    hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)Y, X, X * Z, X, X * Y, 1, op->lrow[1], op->invd[1],
+                                     op->stream), "chol y");
+  // x lines: (y, z) -> base = l*X, stride 1
+  if (X > 1)
+    hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)X, 1, Y * Z, Y * Z, 0, X, op->lrow[0], op->invd[0],
+                                     op->stream), "chol x");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_vec_axpby(gdm_op *op, int64_t n, double a, const double *x, double b, double *y) {
+  if (!op || (n > 0 && (!x || !y))) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  hip_check(gdmk_launch_axpby(n, a, x, b, y, op->stream), "axpby");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_vec_dot(gdm_op *op, int64_t n, const double *x, const double *y, double *result_host) {
+  if (!op || !result_host || (n > 0 && (!x || !y))) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  if (n <= 0) {
+    *result_host = 0.0;
+    return GDM_OK;
+  }
+  const int np = (int)std::min<int64_t>(op->n_dot_partial, std::max<int64_t>(1, (n + 255) / 256));
+  hip_check(gdmk_launch_dot(n, x, y, op->dot_partial, np, op->dot_out, op->stream), "dot");
+  hip_check(hipMemcpyAsync(result_host, op->dot_out, sizeof(double), hipMemcpyDeviceToHost, op->stream), "d2h");
+  hip_check(hipStreamSynchronize(op->stream), "sync");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_synchronize(gdm_op *op) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  hipError_t e = hipStreamSynchronize(op->stream);
+  if (e != hipSuccess) return fail(GDM_ERR_HIP, hipGetErrorString(e));
+  return GDM_OK;
+}
+
+int gdm_malloc(gdm_op *op, size_t bytes, void **ptr) {
+  if (!op || !ptr) return fail(GDM_ERR_ARG, "NULL argument");
+  (void)hipSetDevice(op->device);
+  hipError_t e = hipMalloc(ptr, std::max<size_t>(bytes, 1));
+  if (e != hipSuccess) return fail(GDM_ERR_NOMEM, hipGetErrorString(e));
+  return GDM_OK;
+}
+
+int gdm_free(gdm_op *op, void *ptr) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  (void)hipSetDevice(op->device);
+  hipError_t e = hipFree(ptr);
+  if (e != hipSuccess) return fail(GDM_ERR_HIP, hipGetErrorString(e));
+  return GDM_OK;
+}
+
+int gdm_memcpy_h2d(gdm_op *op, void *dst, const void *src_host, size_t bytes) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  hipError_t e = hipMemcpyAsync(dst, src_host, bytes, hipMemcpyHostToDevice, op->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(op->stream);
+  if (e != hipSuccess) return fail(GDM_ERR_HIP, hipGetErrorString(e));
+  return GDM_OK;
+}
+
+int gdm_memcpy_d2h(gdm_op *op, void *dst_host, const void *src, size_t bytes) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  hipError_t e = hipMemcpyAsync(dst_host, src, bytes, hipMemcpyDeviceToHost, op->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(op->stream);
+  if (e != hipSuccess) return fail(GDM_ERR_HIP, hipGetErrorString(e));
+  return GDM_OK;
+}
+
+int gdm_bc_points(const gdm_op *op, double *xyz_host) {
+  if (!op || !xyz_host) return fail(GDM_ERR_ARG, "NULL argument");
+  const int n1 = op->p + 1;
+  for (const Face &F : op->faces) {
+    const FaceDir *T[2] = {&F.t0, &F.t1};
+    for (int64_t i1 = 0; i1 < F.t1.Q; ++i1)
+      for (int64_t i0 = 0; i0 < F.t0.Q; ++i0) {
+        double *pt = xyz_host + 3 * (F.offset + i1 * F.t0.Q + i0);
+        pt[0] = pt[1] = pt[2] = 0.0;
+        pt[F.d] = F.side ? op->mesh.hi[F.d] : op->mesh.lo[F.d];
+        const int64_t qi[2] = {i0, i1};
+        for (int k = 0; k < 2; ++k) {
+          const int e = T[k]->dim_index;
+          if (e < 0) continue;
+          const int c = T[k]->cell_begin + (int)(qi[k] / n1), qq = (int)(qi[k] % n1);
+          const double h = (op->mesh.hi[e] - op->mesh.lo[e]) / op->mesh.n_subdivisions[e];
+          pt[e] = op->mesh.lo[e] + (c + op->xq[qq]) * h;
+        }
+      }
+  }
+  return GDM_OK;
+}
+
+int gdm_bc_reference_order(const gdm_op *op, int64_t *ref_to_dev_host) {
+  if (!op || !ref_to_dev_host) return fail(GDM_ERR_ARG, "NULL argument");
+  // reference order: owned cells lexicographic, faces 0..2dim-1 at the box,
+  // face points in deal.II QProjector order (stiffness.h:97-157)
+  const int dim = op->dim, n1 = op->p + 1, q = dim - 1;
+  const gdm_layout &L = op->layout;
+  int nc[3] = {1, 1, 1};
+  for (int d = 0; d < dim; ++d) nc[d] = op->mesh.n_subdivisions[d];
+  int cb[3] = {0, 0, 0}, ce[3] = {nc[0], nc[1], nc[2]};
+  cb[q] = L.cell_plane_begin;
+  ce[q] = L.cell_plane_end;
+  const int nfq = dim == 1 ? 1 : (dim == 2 ? n1 : n1 * n1);
+  int64_t k = 0;
+  for (int c2 = cb[2]; c2 < ce[2]; ++c2)
+    for (int c1 = cb[1]; c1 < ce[1]; ++c1)
+      for (int c0 = cb[0]; c0 < ce[0]; ++c0) {
+        const int c[3] = {c0, c1, c2};
+        for (int f = 0; f < 2 * dim; ++f) {
+          const int d = f / 2, side = f % 2;
+          if (!(side ? c[d] == nc[d] - 1 : c[d] == 0)) continue;
+          const Face *F = nullptr;
+          for (const Face &G : op->faces)
+            if (G.d == d && G.side == side) F = &G;
+          if (!F) return fail(GDM_ERR_STATE, "face missing");
+          for (int qi = 0; qi < nfq; ++qi, ++k) {
+            const int aa = qi % n1, bb = qi / n1;
+            int qt0 = 0, qt1 = 0;  // quadrature index along t0 / t1
+            if (dim == 2) {
+              qt0 = aa;
+            } else if (dim == 3) {
+              if (d == 0) { qt0 = aa; qt1 = bb; }       // (0, q0, q1): y <- a, z <- b
+              else if (d == 1) { qt0 = bb; qt1 = aa; }  // (q1, 0, q0): x <- b, z <- a
+              else { qt0 = aa; qt1 = bb; }              // (q0, q1, 0): x <- a, y <- b
+            }
+            int64_t Q0 = 0, Q1 = 0;
+            if (F->t0.dim_index >= 0) Q0 = (int64_t)(c[F->t0.dim_index] - F->t0.cell_begin) * n1 + qt0;
+            if (F->t1.dim_index >= 0) Q1 = (int64_t)(c[F->t1.dim_index] - F->t1.cell_begin) * n1 + qt1;
+            ref_to_dev_host[k] = F->offset + Q1 * F->t0.Q + Q0;
+          }
+        }
+      }
+  if (k != L.n_bc_points) return fail(GDM_ERR_STATE, "boundary point count mismatch");
+  return GDM_OK;
+}
+
+int gdm_time_op(gdm_op *op, int which, const double *src, double *dst, const double *bc_values, int n_iter,
+                double *avg_ms_host) {
+  if (!op || !avg_ms_host || n_iter <= 0) return fail(GDM_ERR_ARG, "bad argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  hipEvent_t e0, e1;
+  hip_check(hipEventCreate(&e0), "event");
+  hip_check(hipEventCreate(&e1), "event");
+  hip_check(hipEventRecord(e0, op->stream), "record");
+  int rc = GDM_OK;
+  for (int i = 0; i < n_iter && rc == GDM_OK; ++i) {
+    if (which == 0) rc = gdm_apply(op, src, dst, bc_values);
+    else if (which == 1) rc = gdm_mass_apply(op, src, dst);
+    else rc = gdm_mass_solve(op, src, dst);
+  }
+  hip_check(hipEventRecord(e1, op->stream), "record");
+  hip_check(hipEventSynchronize(e1), "sync");
+  float ms = 0.f;
+  hip_check(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc != GDM_OK) return rc;
+  *avg_ms_host = ms / n_iter;
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+}  // extern "C"

@@ -1,0 +1,11 @@
+"""gdm_amd -- MI355X-native operator engine for the Galerkin-difference-method
+hot path of peterrum/dealii-galerkin-difference-methods.
+
+Product path: HIP kernels in ../csrc behind the C ABI ../../include/gdm_hip.h
+(libgdm_hip.so), driven from these host-side mirrors of the reference's
+operator classes.  No CPU fallback exists.
+"""
+from ._capi import GdmError, load, declared_symbols, device_count  # noqa: F401
+from .operator import GdmOperator  # noqa: F401
+
+__all__ = ["GdmError", "GdmOperator", "load", "declared_symbols", "device_count"]

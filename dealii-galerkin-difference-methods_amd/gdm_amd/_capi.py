@@ -1,0 +1,123 @@
+"""ctypes binding of libgdm_hip.so (include/gdm_hip.h).
+
+The product path: every device computation goes through these entry points.
+There is no CPU fallback -- if the library or a GPU is missing, operator
+construction raises GdmError.
+"""
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgdm_hip.so")
+HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gdm_hip.h")
+
+GDM_OK = 0
+GDM_OP_MASS, GDM_OP_ADVECTION, GDM_OP_WAVE, GDM_OP_CONVECTIVE = 0, 1, 2, 3
+
+
+class GdmError(RuntimeError):
+    pass
+
+
+class MeshDesc(ctypes.Structure):
+    _fields_ = [
+        ("dim", ctypes.c_int32),
+        ("fe_degree", ctypes.c_int32),
+        ("n_subdivisions", ctypes.c_int32 * 3),
+        ("lo", ctypes.c_double * 3),
+        ("hi", ctypes.c_double * 3),
+        ("n_ranks", ctypes.c_int32),
+        ("rank", ctypes.c_int32),
+        ("periodic", ctypes.c_int32),
+    ]
+
+
+class Layout(ctypes.Structure):
+    _fields_ = [
+        ("n_dofs_global", ctypes.c_int64),
+        ("plane_size", ctypes.c_int64),
+        ("n_planes_global", ctypes.c_int32),
+        ("owned_plane_begin", ctypes.c_int32),
+        ("owned_plane_end", ctypes.c_int32),
+        ("ghost_planes_below", ctypes.c_int32),
+        ("ghost_planes_above", ctypes.c_int32),
+        ("cell_plane_begin", ctypes.c_int32),
+        ("cell_plane_end", ctypes.c_int32),
+        ("halo_depth", ctypes.c_int32),
+        ("n_owned", ctypes.c_int64),
+        ("n_local", ctypes.c_int64),
+        ("n_bc_points", ctypes.c_int64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def load():
+    """Load libgdm_hip.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GdmError("libgdm_hip.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, i32, i64, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+    sig = {
+        "gdm_last_error": [ctypes.c_char_p, ctypes.c_size_t],
+        "gdm_abi_version": [],
+        "gdm_get_device_count": [ctypes.POINTER(ctypes.c_int)],
+        "gdm_op_create": [ctypes.POINTER(MeshDesc), i32, P, i32, i32, ctypes.POINTER(P)],
+        "gdm_op_destroy": [P],
+        "gdm_op_layout": [P, ctypes.POINTER(Layout)],
+        "gdm_op_set_stream": [P, P],
+        "gdm_op_use_own_stream": [P],
+        "gdm_apply": [P, P, P, P],
+        "gdm_add_boundary_data": [P, P, P],
+        "gdm_mass_apply": [P, P, P],
+        "gdm_mass_solve": [P, P, P],
+        "gdm_vec_axpby": [P, i64, d, P, d, P],
+        "gdm_vec_dot": [P, i64, P, P, ctypes.POINTER(d)],
+        "gdm_synchronize": [P],
+        "gdm_malloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
+        "gdm_free": [P, P],
+        "gdm_memcpy_h2d": [P, P, P, ctypes.c_size_t],
+        "gdm_memcpy_d2h": [P, P, P, ctypes.c_size_t],
+        "gdm_bc_points": [P, P],
+        "gdm_bc_reference_order": [P, P],
+        "gdm_time_op": [P, i32, P, P, P, i32, ctypes.POINTER(d)],
+    }
+    for name, args in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(1024)
+    load().gdm_last_error(buf, 1024)
+    return buf.value.decode(errors="replace")
+
+
+def check(rc, what=""):
+    if rc != GDM_OK:
+        raise GdmError("%s failed (%d): %s" % (what, rc, last_error()))
+    return rc
+
+
+def declared_symbols():
+    """Every function the public header declares (for the export test)."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^int\s+(gdm_\w+)\s*\(", txt, flags=re.M)))
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    rc = load().gdm_get_device_count(ctypes.byref(n))
+    return n.value if rc == GDM_OK else 0

@@ -1,0 +1,172 @@
+"""Device operator handle over the C ABI (include/gdm_hip.h).
+
+`GdmOperator` owns one `gdm_op`: the uncut structured-mesh GDM operator of
+one rank (mass, advection, wave or convective) with its slab layout.  Vectors
+are torch CUDA tensors (fp64); torch is only the allocator / stream provider.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _capi
+from ._capi import GdmError, check
+
+KINDS = {
+    "mass": _capi.GDM_OP_MASS,
+    "advection": _capi.GDM_OP_ADVECTION,
+    "wave": _capi.GDM_OP_WAVE,
+    "convective": _capi.GDM_OP_CONVECTIVE,
+}
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    import torch
+
+    if not t.is_cuda or t.dtype != torch.float64:
+        raise GdmError("device fp64 tensor expected")
+    if not t.is_contiguous():
+        raise GdmError("contiguous tensor expected")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class GdmOperator:
+    """One rank's operator.  Local vectors are laid out
+    [ghost planes below | owned planes | ghost planes above] along the last
+    coordinate, each plane in the reference's lexicographic DoF order."""
+
+    def __init__(self, dim, fe_degree, n_subdivisions, lo, hi, kind, params=(), rank=0, n_ranks=1, device=0,
+                 periodic=0):
+        import torch
+
+        self._torch = torch
+        self.lib = _capi.load()
+        if not torch.cuda.is_available():
+            raise GdmError("no GPU visible: the GDM operator engine has no CPU path")
+        m = _capi.MeshDesc()
+        m.dim = dim
+        m.fe_degree = fe_degree
+        ns = list(n_subdivisions) if hasattr(n_subdivisions, "__len__") else [n_subdivisions] * dim
+        los = list(lo) if hasattr(lo, "__len__") else [lo] * dim
+        his = list(hi) if hasattr(hi, "__len__") else [hi] * dim
+        for d in range(3):
+            m.n_subdivisions[d] = int(ns[d]) if d < dim else 1
+            m.lo[d] = float(los[d]) if d < dim else 0.0
+            m.hi[d] = float(his[d]) if d < dim else 1.0
+        m.n_ranks, m.rank, m.periodic = n_ranks, rank, periodic
+        self.mesh = m
+        self.dim, self.p = dim, fe_degree
+        self.kind = KINDS[kind] if isinstance(kind, str) else kind
+        self.device = device
+        arr = (ctypes.c_double * max(1, len(params)))(*params) if len(params) else None
+        h = ctypes.c_void_p()
+        torch.cuda.set_device(device)
+        check(self.lib.gdm_op_create(ctypes.byref(m), self.kind, arr, len(params), device, ctypes.byref(h)),
+              "gdm_op_create")
+        self.h = h
+        lay = _capi.Layout()
+        check(self.lib.gdm_op_layout(self.h, ctypes.byref(lay)), "gdm_op_layout")
+        self.layout = lay.as_dict()
+        self.use_torch_stream()
+
+    # -- lifetime -----------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gdm_op_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def use_torch_stream(self):
+        """Order the operator's launches on torch's current stream."""
+        s = self._torch.cuda.current_stream(self.device).cuda_stream
+        check(self.lib.gdm_op_set_stream(self.h, ctypes.c_void_p(s)), "gdm_op_set_stream")
+
+    # -- layout helpers --------------------------------------------------------
+    @property
+    def n_local(self):
+        return self.layout["n_local"]
+
+    @property
+    def n_owned(self):
+        return self.layout["n_owned"]
+
+    @property
+    def n_bc_points(self):
+        return self.layout["n_bc_points"]
+
+    def owned_view(self, local):
+        lay = self.layout
+        b = lay["ghost_planes_below"] * lay["plane_size"]
+        return local[b:b + lay["n_owned"]]
+
+    def new_vector(self, local=True):
+        n = self.n_local if local else self.n_owned
+        return self._torch.zeros(n, dtype=self._torch.float64, device="cuda:%d" % self.device)
+
+    def _check_sizes(self, src_local, dst_owned):
+        if src_local is not None and src_local.numel() != self.n_local:
+            raise GdmError("src has %d entries, local layout needs %d" % (src_local.numel(), self.n_local))
+        if dst_owned is not None and dst_owned.numel() != self.n_owned:
+            raise GdmError("dst has %d entries, owned layout needs %d" % (dst_owned.numel(), self.n_owned))
+
+    # -- operator applications -------------------------------------------------
+    def apply(self, src_local, dst_owned, bc_values=None):
+        self._check_sizes(src_local, dst_owned)
+        if bc_values is not None and bc_values.numel() != self.n_bc_points:
+            raise GdmError("bc_values has %d entries, expected %d" % (bc_values.numel(), self.n_bc_points))
+        check(self.lib.gdm_apply(self.h, _ptr(src_local), _ptr(dst_owned), _ptr(bc_values)), "gdm_apply")
+        return dst_owned
+
+    def add_boundary_data(self, bc_values, dst_owned):
+        self._check_sizes(None, dst_owned)
+        check(self.lib.gdm_add_boundary_data(self.h, _ptr(bc_values), _ptr(dst_owned)), "gdm_add_boundary_data")
+        return dst_owned
+
+    def mass_apply(self, src_local, dst_owned):
+        self._check_sizes(src_local, dst_owned)
+        check(self.lib.gdm_mass_apply(self.h, _ptr(src_local), _ptr(dst_owned)), "gdm_mass_apply")
+        return dst_owned
+
+    def mass_solve(self, rhs_owned, x_owned):
+        self._check_sizes(None, rhs_owned)
+        self._check_sizes(None, x_owned)
+        check(self.lib.gdm_mass_solve(self.h, _ptr(rhs_owned), _ptr(x_owned)), "gdm_mass_solve")
+        return x_owned
+
+    def axpby(self, a, x, b, y):
+        check(self.lib.gdm_vec_axpby(self.h, x.numel(), float(a), _ptr(x), float(b), _ptr(y)), "gdm_vec_axpby")
+        return y
+
+    def dot(self, x, y):
+        r = ctypes.c_double(0.0)
+        check(self.lib.gdm_vec_dot(self.h, x.numel(), _ptr(x), _ptr(y), ctypes.byref(r)), "gdm_vec_dot")
+        return r.value
+
+    def synchronize(self):
+        check(self.lib.gdm_synchronize(self.h), "gdm_synchronize")
+
+    def time_op(self, which, src, dst, bc=None, n_iter=10):
+        ms = ctypes.c_double(0.0)
+        check(self.lib.gdm_time_op(self.h, int(which), _ptr(src), _ptr(dst), _ptr(bc), int(n_iter), ctypes.byref(ms)),
+              "gdm_time_op")
+        return ms.value
+
+    # -- boundary points -------------------------------------------------------
+    def bc_points(self):
+        n = self.n_bc_points
+        xyz = np.zeros((max(n, 1), 3))
+        check(self.lib.gdm_bc_points(self.h, xyz.ctypes.data_as(ctypes.c_void_p)), "gdm_bc_points")
+        return xyz[:n]
+
+    def bc_reference_order(self):
+        n = self.n_bc_points
+        perm = np.zeros(max(n, 1), dtype=np.int64)
+        check(self.lib.gdm_bc_reference_order(self.h, perm.ctypes.data_as(ctypes.c_void_p)),
+              "gdm_bc_reference_order")
+        return perm[:n]

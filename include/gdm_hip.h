@@ -1,0 +1,169 @@
+/*
+ * gdm_hip.h -- C ABI of libgdm_hip.so, the MI355X (gfx950) operator engine for
+ * the Galerkin-difference-method (GDM) hot path of
+ * peterrum/dealii-galerkin-difference-methods.
+ *
+ * The reference has no formal FFI: its drop-in surface is the operator classes
+ * the RK drivers call plus deal.II's MatrixType concept (vmult).  Each entry
+ * point below replaces one of those reference interfaces (paths relative to
+ * the reference root):
+ *
+ *   gdm_op_create        GDM::System<dim>(comm, p, n_comp, ghost) +
+ *                        subdivided_hyper_cube + categorize
+ *                        (include/gdm/system.h:355-424) and
+ *                        Discretization::reinit
+ *                        (applications/advection/include/gdm/advection/
+ *                        discretization.h:27-89) and
+ *                        StiffnessMatrixOperator::reinit (advection/stiffness.h:23-38,
+ *                        wave/stiffness.h:23-31) / MassMatrixOperator::reinit
+ *                        (advection/mass.h:25-28)
+ *   gdm_op_layout        System::locally_owned_dofs / locally_active_dofs and the
+ *                        Partitioner (system.h:634-688, 720-757;
+ *                        advection/discretization.h:85-88), plus
+ *                        StiffnessMatrixOperator::initialize_dof_vector's block(0)
+ *                        size (advection/stiffness.h:162-179)
+ *   gdm_apply            StiffnessMatrixOperator::compute_rhs (advection:
+ *                        advection/stiffness.h:196-606; wave:
+ *                        wave/stiffness.h:409-420 -> :42-407), volume + box-face
+ *                        terms of the uncut path
+ *   gdm_mass_apply       TrilinosWrappers::SparseMatrix::vmult on the matrix of
+ *                        MassMatrixOperator::get_sparse_matrix (advection/mass.h:30-36)
+ *   gdm_mass_solve       *Problem::solve(mass_matrix, result, rhs)
+ *                        (advection/problem.h:236-267, wave/problem.h:471-502):
+ *                        the CG + ILU/AMG solve is replaced by the exact
+ *                        Kronecker inverse of the uncut mass matrix
+ *   gdm_vec_axpby/dot    the vector updates of TimeStepping::ExplicitRungeKutta
+ *                        (advection/problem.h:91-94) / SolverCG inner products
+ *   gdm_bc_points        StiffnessMatrixOperator::collect_boundary_points
+ *                        (advection/stiffness.h:40-160): coordinates of the
+ *                        boundary quadrature points (device order)
+ *   gdm_bc_reference_order  permutation between the reference's block(0)
+ *                        order (cell, face, q) and the device order
+ *
+ * Conventions: plain pointers and sizes only; every function returns GDM_OK (0)
+ * or a negative error code, never throws across the ABI; the message of the
+ * last error on the calling thread is available from gdm_last_error.  Vector
+ * arguments are DEVICE pointers (hipMalloc'ed or torch CUDA tensors) unless
+ * the name says _host.  Calls are ordered on the operator's stream; results
+ * that reach host memory are synchronous on return.
+ */
+#ifndef GDM_HIP_H
+#define GDM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GDM_HIP_ABI_VERSION 1
+
+enum gdm_status {
+  GDM_OK = 0,
+  GDM_ERR_ARG = -1,         /* invalid argument (AssertThrow in the reference) */
+  GDM_ERR_HIP = -2,         /* HIP runtime error */
+  GDM_ERR_UNSUPPORTED = -3, /* ExcNotImplemented in the reference */
+  GDM_ERR_NOMEM = -4,
+  GDM_ERR_STATE = -5
+};
+
+/* operator kinds */
+enum gdm_op_kind {
+  GDM_OP_MASS = 0,       /* (v, u)                                  mass.h:144-156   */
+  GDM_OP_ADVECTION = 1,  /* (a u, grad v) - <(a.n) u_up, v>_box     stiffness.h:345-532 */
+  GDM_OP_WAVE = 2,       /* -(grad v, grad u) [+ Nitsche on the box] wave/stiffness.h:151-330 */
+  GDM_OP_CONVECTIVE = 3  /* -(a . grad u, v)  prototypes/advection_01_gdm.cc:164-206 */
+};
+
+typedef struct gdm_op gdm_op;
+
+typedef struct {
+  int32_t dim;               /* 1, 2 or 3                                   */
+  int32_t fe_degree;         /* odd, 1..9 (fe.h:321-323)                     */
+  int32_t n_subdivisions[3]; /* cells per direction                          */
+  double lo[3], hi[3];       /* box (subdivided_hyper_cube/_rectangle)       */
+  int32_t n_ranks, rank;     /* slab partition along the last coordinate     */
+  int32_t periodic;          /* bit d: periodic constraints in direction d   */
+} gdm_mesh_desc;
+
+/* Local vector layout of one rank.  Device vectors are stored
+ * [ghost planes below | owned planes | ghost planes above], each plane
+ * lexicographic (x fastest), i.e. the reference's global DoF order
+ * (system.h:238-244) restricted to a plane range. */
+typedef struct {
+  int64_t n_dofs_global;
+  int64_t plane_size;             /* DoFs per vertex plane of the last coordinate */
+  int32_t n_planes_global;
+  int32_t owned_plane_begin;      /* global vertex planes [begin, end) owned   */
+  int32_t owned_plane_end;
+  int32_t ghost_planes_below;     /* halo depth actually present (<= p)         */
+  int32_t ghost_planes_above;
+  int32_t cell_plane_begin;       /* owned cell planes (system.h:747-757)       */
+  int32_t cell_plane_end;
+  int32_t halo_depth;             /* = fe_degree                                */
+  int64_t n_owned;                /* owned DoFs                                 */
+  int64_t n_local;                /* owned + ghost DoFs                         */
+  int64_t n_bc_points;            /* block(0) size (boundary points of owned cells) */
+} gdm_layout;
+
+/* params (n_params):
+ *   GDM_OP_MASS        : none
+ *   GDM_OP_ADVECTION   : a_x, a_y, a_z               (constant field)
+ *   GDM_OP_CONVECTIVE  : a_x, a_y, a_z
+ *   GDM_OP_WAVE        : [nitsche_parameter]         (> 0 enables box Nitsche,
+ *                        function_domain_dbc; absent / <= 0 = natural BC) */
+int gdm_last_error(char *buf, size_t len);
+int gdm_abi_version(void);
+int gdm_get_device_count(int *n);
+
+int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int n_params, int device,
+                  gdm_op **out);
+int gdm_op_destroy(gdm_op *op);
+int gdm_op_layout(const gdm_op *op, gdm_layout *out);
+/* launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream;
+ * NULL is the HIP null stream); gdm_op_use_own_stream restores the operator's
+ * private non-blocking stream */
+int gdm_op_set_stream(gdm_op *op, void *hip_stream);
+int gdm_op_use_own_stream(gdm_op *op);
+
+/* dst_owned = K src_local (+ inflow boundary-data term when bc_values != NULL,
+ * advection only: bc_values are the stage boundary values, device order, size
+ * n_bc_points).  src_local has the full local layout (ghost planes filled). */
+int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const double *bc_values);
+/* dst_owned += inflow boundary-data term only (the bc part of gdm_apply,
+ * advection/stiffness.h:520-529 with a.n < 0); no-op for other kinds */
+int gdm_add_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned);
+/* dst_owned = M src_local */
+int gdm_mass_apply(gdm_op *op, const double *src_local, double *dst_owned);
+/* x_owned = M^-1 rhs_owned (exact Kronecker inverse; single rank) */
+int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned);
+
+/* y = a x + b y ; *result_host = x . y */
+int gdm_vec_axpby(gdm_op *op, int64_t n, double a, const double *x, double b, double *y);
+int gdm_vec_dot(gdm_op *op, int64_t n, const double *x, const double *y, double *result_host);
+int gdm_synchronize(gdm_op *op);
+
+/* memory helpers for callers without their own device allocator */
+int gdm_malloc(gdm_op *op, size_t bytes, void **ptr);
+int gdm_free(gdm_op *op, void *ptr);
+int gdm_memcpy_h2d(gdm_op *op, void *dst, const void *src_host, size_t bytes);
+int gdm_memcpy_d2h(gdm_op *op, void *dst_host, const void *src, size_t bytes);
+
+/* boundary points of the owned cells: coordinates (n_bc_points x 3, device
+ * order) and ref_to_dev[i] = device index of the i-th point in the
+ * reference's block(0) order (cells lexicographic, faces 0..2dim-1, q). */
+int gdm_bc_points(const gdm_op *op, double *xyz_host);
+int gdm_bc_reference_order(const gdm_op *op, int64_t *ref_to_dev_host);
+
+/* time n_iter back-to-back applications with HIP events on the operator's
+ * stream; which: 0 = gdm_apply, 1 = gdm_mass_apply, 2 = gdm_mass_solve.
+ * avg_ms_host receives the mean time per application. */
+int gdm_time_op(gdm_op *op, int which, const double *src, double *dst, const double *bc_values, int n_iter,
+                double *avg_ms_host);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GDM_HIP_H */
