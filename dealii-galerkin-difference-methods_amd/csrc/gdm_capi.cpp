@@ -82,7 +82,9 @@ struct gdm_op {
   double a[3] = {0, 0, 0};
   double nitsche = 0.0;
   // device tables
-  double *rowMx = nullptr, *rowBx = nullptr, *colMy = nullptr, *colBy = nullptr, *colMz = nullptr, *colBz = nullptr;
+  double *tMx = nullptr, *tBx = nullptr, *corrX = nullptr;
+  int x_corr_left = 0, x_corr_right = 0;
+  double *colMy = nullptr, *colBy = nullptr, *colMz = nullptr, *colBz = nullptr;
   double *lrow[3] = {nullptr, nullptr, nullptr}, *invd[3] = {nullptr, nullptr, nullptr};
   std::vector<Face> faces;
   double *face_tmp = nullptr;
@@ -113,8 +115,6 @@ T *keep(gdm_op *op, T *ptr) {
 
 // Build the row (x) or column (y, z) band table of a kernel axis in kernel
 // order.  For column tables entry [s][k] holds A(s - p + k, s).
-std::vector<double> band_rows(const gdm::Band &A) { return A.a; }
-
 std::vector<double> band_cols(const gdm::Band &A, int pad, int pad_back) {
   // rows [0, pad) and [pad + n, pad + n + pad_back) are zero: the kernel reads
   // them for halo rows outside the domain and for rows of a partial last tile
@@ -197,8 +197,35 @@ void build_tables(gdm_op *op) {
     }
     B[ax] = b;
   }
-  op->rowMx = keep(op, dev_upload(band_rows(M[0])));
-  op->rowBx = keep(op, dev_upload(band_rows(B[0])));
+  // x: wave-uniform Toeplitz row + corrections of the p+1 wall columns on
+  // each side (rows x <= p and x >= n - p involve the one-sided categories)
+  {
+    const int n = M[0].n, W = 2 * p + 1;
+    std::vector<double> tM(W, 0.0), tB(W, 0.0);
+    const bool has_interior = n >= 2 * p + 3;
+    if (has_interior) {
+      const int xi = n / 2;
+      for (int k = 0; k < W; ++k) {
+        tM[k] = M[0](xi, xi - p + k);
+        tB[k] = B[0](xi, xi - p + k);
+      }
+    }
+    op->x_corr_left = std::min(p + 1, n);
+    const int right_begin = std::max(p + 1, n - p - 1);
+    op->x_corr_right = std::max(0, n - right_begin);
+    std::vector<double> corr((size_t)2 * (p + 1) * 2 * W, 0.0);
+    auto fill = [&](int slot, int x) {
+      for (int k = 0; k < W; ++k) {
+        corr[(size_t)slot * 2 * W + k] = M[0](x, x - p + k) - tM[k];
+        corr[(size_t)slot * 2 * W + W + k] = B[0](x, x - p + k) - tB[k];
+      }
+    };
+    for (int x = 0; x < op->x_corr_left; ++x) fill(x, x);
+    for (int j = 0; j < op->x_corr_right; ++j) fill(p + 1 + j, right_begin + j);
+    op->tMx = keep(op, dev_upload(tM));
+    op->tBx = keep(op, dev_upload(tB));
+    op->corrX = keep(op, dev_upload(corr));
+  }
   const int ypad = p + 64;  // >= p + max tile rows
   op->colMy = keep(op, dev_upload(band_cols(M[1], p, ypad)));
   op->colBy = keep(op, dev_upload(band_cols(B[1], p, ypad)));
@@ -336,8 +363,11 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst)
     a.out_z0 = 0; a.out_z1 = 1; a.out_y0 = L.owned_plane_begin; a.out_y1 = L.owned_plane_end;
   }
   a.zchunk = std::max(1, std::min(op->zchunk, a.out_z1 - a.out_z0));
-  a.rowMx = op->rowMx;
-  a.rowBx = op->rowBx;
+  a.tMx = op->tMx;
+  a.tBx = op->tBx;
+  a.corrX = op->corrX;
+  a.x_corr_left = op->x_corr_left;
+  a.x_corr_right = op->x_corr_right;
   a.colMy = op->colMy;
   a.colBy = op->colBy;
   a.colMz = op->colMz;

@@ -15,8 +15,12 @@ struct StencilArgs {
   int in_y0, in_y1, in_z0, in_z1;      // valid input box (global indices)
   int out_y0, out_y1, out_z0, out_z1;  // output box
   int zchunk;                          // output planes per workgroup
-  const double *__restrict__ rowMx;    // [Nx][2p+1]      M_x(x, x - p + k)
-  const double *__restrict__ rowBx;    // [Nx][2p+1]
+  const double *__restrict__ tMx;      // [2p+1] Toeplitz (interior) row of M_x
+  const double *__restrict__ tBx;      // [2p+1] Toeplitz (interior) row of B_x
+  const double *__restrict__ corrX;    // [2(p+1)][2 (2p+1)] (row_M(x) - tM, row_B(x) - tB) of the wall
+                                       //   columns: slot x for x < x_corr_left, slot p+1+j for
+                                       //   column Nx - x_corr_right + j
+  int x_corr_left, x_corr_right;       // wall columns with corrections (<= p+1 each)
   const double *__restrict__ colMy;    // [Ny + 2p][2p+1] row s + p: M_y(s - p + k, s)
   const double *__restrict__ colBy;
   const double *__restrict__ colMz;    // [Nz][2p+1]      M_z(z - p + k, z)

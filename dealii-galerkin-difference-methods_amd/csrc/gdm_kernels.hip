@@ -19,6 +19,7 @@
 // per-lane registers (they differ only near the x faces).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "gdm_kernels.h"
 
@@ -26,43 +27,230 @@ namespace gdmk {
 
 
 
-template <int P, int R, int NW>
+template <int P, int R, int NW, int NBUF_ = 3, int WPC_ = 2>
 struct StencilGeom {
-  static constexpr int W = 2 * P + 1;  // band width = ring size
-  static constexpr int TX = 64;        // one wave row
-  static constexpr int TY = R * NW;
-  static constexpr int UR = TY + 2 * P;  // staged rows
-  static constexpr int UP = TX + 2 * P;  // staged row pitch (doubles)
+  static constexpr int W = 2 * P + 1;      // band width = ring size
+  static constexpr int TX = 64;            // one wave row
+  static constexpr int TY = R * NW;        // output rows per tile
+  static constexpr int UR = TY + 2 * P;    // staged rows
+  static constexpr int XH = (P + 1) & ~1;  // x halo, even -> 16-B aligned row start
+  static constexpr int RL = TX + 2 * XH;   // staged row length (doubles)
   static constexpr int NT = 64 * NW;
+  static constexpr int NBUF = NBUF_;       // plane ring: current + NBUF-1 in flight
+  static constexpr int WPC = WPC_;         // resident workgroups per CU (register budget)
+  static constexpr int NCORR = 2 * (P + 1);  // x columns whose band row differs from the Toeplitz row
+  static constexpr int USZ = UR * RL;      // doubles per staged plane
   static constexpr size_t lds_bytes(bool mass) {
-    return sizeof(double) * ((size_t)UR * UP + (size_t)UR * TX * (mass ? 1 : 2));
+    return sizeof(double) * ((size_t)NBUF * USZ + (size_t)UR * TX * (mass ? 1 : 2) + (size_t)NCORR * 2 * W);
   }
 };
 
-template <int P, int R, int NW, bool MASS>
-__global__ void __launch_bounds__(64 * NW) stencil3d_kernel(StencilArgs a) {
+// Stage one plane tile (rows y0-P .. y0+TY+P-1, columns x0-XH .. x0+TX+XH-1)
+// into LDS with LDS-DMA (buffer_load ... lds).  Chunks outside the valid
+// input box get an out-of-range voffset, which the buffer range check turns
+// into zeros.  CH = 16 (2 doubles per lane; rows 16-B aligned: Nx even) or
+// CH = 4 (any Nx).
+template <int P, int R, int NW, int CH>
+struct StageCount {
   using G = StencilGeom<P, R, NW>;
-  constexpr int W = G::W, TX = G::TX, TY = G::TY, UR = G::UR, UP = G::UP, NT = G::NT;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  double *us = smem;              // UR x UP
-  double *as = smem + UR * UP;    // UR x TX
-  double *bs = as + UR * TX;      // UR x TX (unused for MASS)
+  static constexpr int DPC = CH / 4;                 // dwords per chunk
+  static constexpr int CPR = G::RL * 2 / DPC;        // chunks per row
+  static constexpr int NCH = G::UR * CPR;            // chunks per plane
+  static constexpr int NI = (NCH + 63) / 64;         // wave-instructions per plane
+  static constexpr int MIN_PER_WAVE = NI / NW;       // issued by every wave
+};
 
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int x0 = blockIdx.x * TX;
-  const int y0 = a.out_y0 + blockIdx.y * TY;
-  const int zc0 = a.out_z0 + blockIdx.z * a.zchunk;
-  const int zc1 = min(zc0 + a.zchunk, a.out_z1);
-  const int x = x0 + lane;
-  const int Nx = a.Nx;
-  const int ny_in = a.in_y1 - a.in_y0, ny_out = a.out_y1 - a.out_y0;
+template <int P, int R, int NW, int CH>
+__device__ __forceinline__ void stage_plane(const StencilArgs &a, int zz, int x0, int y0, double *ubuf, int wv,
+                                            int lane) {
+  using G = StencilGeom<P, R, NW>;
+  using SC = StageCount<P, R, NW, CH>;
+  const int ny_in = a.in_y1 - a.in_y0;
+  const double *plane = a.src + (int64_t)(zz - a.in_z0) * ny_in * a.Nx;
+  const int nbytes = (int)((int64_t)ny_in * a.Nx * 8);
+  __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)plane, 0, nbytes, 0x00020000);
+  for (int j = wv; j < SC::NI; j += NW) {
+    const int e = j * 64 + lane;
+    const int r = e / SC::CPR, c = e - r * SC::CPR;
+    const int gy = y0 - P + r;
+    const int gx2 = (x0 - G::XH) * 2 + c * SC::DPC;  // dword column
+    uint32_t voff = 0x80000000u;                      // out of range -> zeros
+    if (e < SC::NCH && gy >= a.in_y0 && gy < a.in_y1 && gx2 >= 0 && gx2 < 2 * a.Nx)
+      voff = (uint32_t)(((int64_t)(gy - a.in_y0) * a.Nx * 2 + gx2) * 4);
+    if (e < SC::NCH) {
+      auto *dst = (__attribute__((address_space(3))) void *)((char *)ubuf + (size_t)j * 64 * CH);
+      if constexpr (CH == 16)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, voff, 0, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, voff, 0, 0, 0);
+    }
+  }
+}
 
-  double cmx[W], cbx[W];
+#define GDM_WAIT_VMCNT(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
+#define GDM_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+// Coefficient tables are read-only for the whole launch and indexed by
+// wave-uniform positions: read them through the constant address space so
+// they become scalar (s_load) loads instead of vector loads.
+typedef __attribute__((address_space(4))) const double cdouble;
+__device__ __forceinline__ cdouble *cptr(const double *p) { return (cdouble *)(p); }
+
+// Per-workgroup state of the z-march (all wave-uniform except lane/x).
+struct MarchCtx {
+  double *ubase, *as, *bs, *corr;
+  int lane, wv, x0, y0, x, zc0, zc1, zs, ze, zend, ybase, cslot, ny_out;
+  bool need_corr;
+};
+
+// One input plane zz at ring phase JP (= zz mod W): stage/sweep/scatter, then
+// retire output plane zz - p.  JP is a template parameter so every ring slot
+// index is a compile-time constant and the ring stays in registers.
+template <int JP, int P, int R, int NW, int NBUF, int WPC, bool MASS, int CH>
+__device__ __forceinline__ void march_plane(const StencilArgs &a, const MarchCtx &c, double (&acc)[2 * P + 1][R],
+                                            int zz) {
+  using G = StencilGeom<P, R, NW, NBUF, WPC>;
+  using SC = StageCount<P, R, NW, CH>;
+  constexpr int W = G::W, TX = G::TX, UR = G::UR, RL = G::RL, XH = G::XH, USZ = G::USZ;
+  if (zz < c.ze) {
+    // ---- 1. this wave's DMA of plane zz landed; barrier: every wave's did
+    //         and every wave finished plane zz-1 ----
+    if (zz + 1 < c.ze)
+      GDM_WAIT_VMCNT(SC::MIN_PER_WAVE);
+    else
+      GDM_WAIT_VMCNT(0);
+    GDM_LDS_BARRIER();
+    // buffer (zz+NBUF-1) % NBUF == (zz-1) % NBUF was last read by the x-sweep of zz-1
+    if (zz + NBUF - 1 < c.ze)
+      stage_plane<P, R, NW, CH>(a, zz + NBUF - 1, c.x0, c.y0, c.ubase + ((zz + NBUF - 1) % NBUF) * USZ, c.wv,
+                                c.lane);
+    const double *us = c.ubase + (zz % NBUF) * USZ;
+    // ---- 2. x-sweep: A = M_x u, Bv = B_x u on the UR staged rows ----
+    // (the Toeplitz row is re-read from the scalar cache every plane instead
+    //  of pinning 4(2p+1) SGPRs for the whole kernel)
+    cdouble *tM = cptr(a.tMx), *tB = cptr(a.tBx);
+    asm volatile("" : "+s"(tM), "+s"(tB));
+    for (int r = c.wv; r < UR; r += NW) {
+      const double *ur = us + r * RL + c.lane + (XH - P);
+      double uk[W];
 #pragma unroll
-  for (int k = 0; k < W; ++k) {
-    cmx[k] = (x < Nx) ? a.rowMx[(size_t)x * W + k] : 0.0;
-    cbx[k] = (!MASS && x < Nx) ? a.rowBx[(size_t)x * W + k] : 0.0;
+      for (int k = 0; k < W; ++k) uk[k] = ur[k];
+      double am = 0.0, ab = 0.0;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        am = fma(tM[k], uk[k], am);
+        if (!MASS) ab = fma(tB[k], uk[k], ab);
+      }
+      if (c.need_corr && c.cslot >= 0) {
+        const double *cm = c.corr + c.cslot * 2 * W;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          am = fma(cm[k], uk[k], am);
+          if (!MASS) ab = fma(cm[W + k], uk[k], ab);
+        }
+      }
+      c.as[r * TX + c.lane] = am;
+      if (!MASS) c.bs[r * TX + c.lane] = ab;
+    }
+    GDM_LDS_BARRIER();
+    // ---- 3. y-sweep: scatter the R + 2p staged rows into this wave's R rows ----
+    double D[R], E[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) D[j] = E[j] = 0.0;
+#pragma unroll
+    for (int t = 0; t < R + 2 * P; ++t) {
+      const int trow = c.wv * R + t;  // tile row
+      const int s = c.ybase - P + t;  // global row, in [-P, Ny + P + TY)
+      const double av = c.as[trow * TX + c.lane];
+      const double bv = MASS ? 0.0 : c.bs[trow * TX + c.lane];
+      cdouble *cm = cptr(a.colMy) + (size_t)(s + P) * W;
+      cdouble *cb = cptr(a.colBy) + (size_t)(s + P) * W;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int k = j + 2 * P - t;
+        if (k >= 0 && k < W) {
+          const double m = cm[k];
+          D[j] = fma(m, av, D[j]);
+          if (!MASS) E[j] = fma(m, bv, fma(cb[k], av, E[j]));
+        }
+      }
+    }
+    // ---- 4. z-scatter into the register ring ----
+    cdouble *cmz = cptr(a.colMz) + (size_t)zz * W;
+    cdouble *cbz = cptr(a.colBz) + (size_t)zz * W;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      constexpr int base = JP - P + 2 * W;
+      const int slot = (base + k) % W;
+      const double m = cmz[k];
+      if (MASS) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc[slot][j] = fma(m, D[j], acc[slot][j]);
+      } else {
+        const double b = cbz[k];
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc[slot][j] = fma(m, E[j], fma(b, D[j], acc[slot][j]));
+      }
+    }
+  }
+  // ---- retire output plane zz - p (complete: every contributing plane done) ----
+  constexpr int rslot = (JP - P + 2 * W) % W;
+  const int zo = zz - P;
+  if (zo >= c.zc0 && zo < c.zc1) {
+    const int Nx = a.Nx;
+    double *orow = a.dst + ((int64_t)(zo - a.out_z0) * c.ny_out + (c.ybase - a.out_y0)) * Nx + c.x;
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (c.x < Nx && c.ybase + j < a.out_y1) orow[(int64_t)j * Nx] = acc[rslot][j];
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
+}
+
+template <int JP, int P, int R, int NW, int NBUF, int WPC, bool MASS, int CH>
+__device__ __forceinline__ void march_phases(const StencilArgs &a, const MarchCtx &c, double (&acc)[2 * P + 1][R],
+                                             int zb) {
+  if constexpr (JP < 2 * P + 1) {
+    const int zz = zb + JP;
+    if (zz >= c.zs && zz < c.zend) march_plane<JP, P, R, NW, NBUF, WPC, MASS, CH>(a, c, acc, zz);
+    march_phases<JP + 1, P, R, NW, NBUF, WPC, MASS, CH>(a, c, acc, zb);
+  }
+}
+
+template <int P, int R, int NW, int NBUF, int WPC, bool MASS, int CH>
+__global__ void __launch_bounds__(64 * NW, (64 * NW * WPC) / 256) stencil3d_kernel(StencilArgs a) {
+  using G = StencilGeom<P, R, NW, NBUF, WPC>;
+  constexpr int W = G::W, TX = G::TX, UR = G::UR, USZ = G::USZ;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  MarchCtx c;
+  c.ubase = smem;                                // NBUF x UR x RL
+  c.as = smem + NBUF * USZ;                      // UR x TX
+  c.bs = c.as + UR * TX;                         // UR x TX (unused for MASS)
+  c.corr = c.as + UR * TX * (MASS ? 1 : 2);      // NCORR x 2W wall-row corrections
+  c.lane = threadIdx.x & 63;
+  c.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.x0 = blockIdx.x * TX;
+  c.y0 = a.out_y0 + blockIdx.y * G::TY;
+  c.zc0 = a.out_z0 + blockIdx.z * a.zchunk;
+  c.zc1 = min(c.zc0 + a.zchunk, a.out_z1);
+  c.x = c.x0 + c.lane;
+  c.ny_out = a.out_y1 - a.out_y0;
+  c.zs = max(c.zc0 - P, a.in_z0);
+  c.ze = min(c.zc1 + P, a.in_z1);  // input planes with contributions: [zs, ze)
+  c.zend = c.zc1 + P;              // retire up to output plane zc1 - 1
+  c.ybase = c.y0 + c.wv * R;       // first output row of this wave
+
+  // x rows: wave-uniform Toeplitz row; the p+1 columns next to each wall
+  // (every column of a domain narrower than 2p + 3) add row(x) - T from a
+  // per-tile LDS table
+  c.need_corr = (c.x0 < a.x_corr_left) || (c.x0 + TX > a.Nx - a.x_corr_right);
+  c.cslot = -1;
+  if (c.need_corr) {
+    if (c.x < a.x_corr_left)
+      c.cslot = c.x;
+    else if (c.x < a.Nx && c.x >= a.Nx - a.x_corr_right)
+      c.cslot = (P + 1) + (c.x - (a.Nx - a.x_corr_right));
+    for (int e = threadIdx.x; e < G::NCORR * 2 * W; e += G::NT) c.corr[e] = a.corrX[e];
   }
 
   double acc[W][R];
@@ -71,97 +259,14 @@ __global__ void __launch_bounds__(64 * NW) stencil3d_kernel(StencilArgs a) {
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
 
-  const int zs = max(zc0 - P, a.in_z0);
-  const int ze = min(zc1 + P, a.in_z1);  // input planes with contributions: [zs, ze)
-  const int zend = zc1 + P;              // retire up to output plane zc1 - 1
-  const int ybase = y0 + wv * R;         // first output row of this wave
+  // prologue: NBUF-1 planes in flight
+#pragma unroll
+  for (int d = 0; d < NBUF - 1; ++d)
+    if (c.zs + d < c.ze)
+      stage_plane<P, R, NW, CH>(a, c.zs + d, c.x0, c.y0, c.ubase + ((c.zs + d) % NBUF) * USZ, c.wv, c.lane);
 
-  for (int zb = zs - (zs % W); zb < zend; zb += W) {
-#pragma unroll
-    for (int jp = 0; jp < W; ++jp) {
-      const int zz = zb + jp;
-      if (zz >= zs && zz < zend) {
-        if (zz < ze) {
-          // ---- 1. stage the plane tile (zero outside the valid input box) ----
-          const double *plane = a.src + (int64_t)(zz - a.in_z0) * ny_in * Nx;
-          for (int e = threadIdx.x; e < UR * UP; e += NT) {
-            const int r = e / UP, c = e - r * UP;
-            const int gx = x0 - P + c, gy = y0 - P + r;
-            double v = 0.0;
-            if (gx >= 0 && gx < Nx && gy >= a.in_y0 && gy < a.in_y1)
-              v = plane[(int64_t)(gy - a.in_y0) * Nx + gx];
-            us[e] = v;
-          }
-          __syncthreads();
-          // ---- 2. x-sweep ----
-          for (int r = wv; r < UR; r += NW) {
-            const double *ur = us + r * UP + lane;
-            double am = 0.0, ab = 0.0;
-#pragma unroll
-            for (int k = 0; k < W; ++k) {
-              const double u = ur[k];
-              am = fma(cmx[k], u, am);
-              if (!MASS) ab = fma(cbx[k], u, ab);
-            }
-            as[r * TX + lane] = am;
-            if (!MASS) bs[r * TX + lane] = ab;
-          }
-          __syncthreads();
-          // ---- 3. y-sweep (scatter into this wave's R rows) ----
-          double D[R], E[R];
-#pragma unroll
-          for (int j = 0; j < R; ++j) D[j] = E[j] = 0.0;
-#pragma unroll
-          for (int t = 0; t < R + 2 * P; ++t) {
-            const int trow = wv * R + t;        // tile row
-            const int s = ybase - P + t;        // global row, in [-P, Ny + P)
-            const double av = as[trow * TX + lane];
-            const double bv = MASS ? 0.0 : bs[trow * TX + lane];
-            const double *cm = a.colMy + (size_t)(s + P) * W;
-            const double *cb = a.colBy + (size_t)(s + P) * W;
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-              const int k = j + 2 * P - t;
-              if (k >= 0 && k < W) {
-                const double m = cm[k];
-                D[j] = fma(m, av, D[j]);
-                if (!MASS) E[j] = fma(m, bv, fma(cb[k], av, E[j]));
-              }
-            }
-          }
-          // ---- 4. z-scatter into the register ring ----
-          const double *cmz = a.colMz + (size_t)zz * W;
-          const double *cbz = a.colBz + (size_t)zz * W;
-#pragma unroll
-          for (int k = 0; k < W; ++k) {
-            const int slot = ((jp - P + k) % W + W) % W;
-            const double m = cmz[k];
-            if (MASS) {
-#pragma unroll
-              for (int j = 0; j < R; ++j) acc[slot][j] = fma(m, D[j], acc[slot][j]);
-            } else {
-              const double b = cbz[k];
-#pragma unroll
-              for (int j = 0; j < R; ++j) acc[slot][j] = fma(m, E[j], fma(b, D[j], acc[slot][j]));
-            }
-          }
-        }
-        // ---- retire output plane zz - P ----
-        {
-          const int slot = ((jp - P) % W + W) % W;
-          const int zo = zz - P;
-          if (zo >= zc0 && zo < zc1) {
-            double *orow = a.dst + ((int64_t)(zo - a.out_z0) * ny_out + (ybase - a.out_y0)) * Nx + x;
-#pragma unroll
-            for (int j = 0; j < R; ++j)
-              if (x < Nx && ybase + j < a.out_y1) orow[(int64_t)j * Nx] = acc[slot][j];
-          }
-#pragma unroll
-          for (int j = 0; j < R; ++j) acc[slot][j] = 0.0;
-        }
-      }
-    }
-  }
+  for (int zb = c.zs - (c.zs % W); zb < c.zend; zb += W)
+    march_phases<0, P, R, NW, NBUF, WPC, MASS, CH>(a, c, acc, zb);
 }
 
 // ---------------------------------------------------------------------------
@@ -305,13 +410,13 @@ __global__ void __launch_bounds__(256) zero_kernel(int64_t n, double *__restrict
 // ---------------------------------------------------------------------------
 // host-side launchers (called from gdm_capi.cpp)
 // ---------------------------------------------------------------------------
-template <int P, int R, int NW, bool MASS>
+template <int P, int R, int NW, int NBUF, int WPC, bool MASS, int CH>
 static hipError_t launch_stencil_t(const StencilArgs &a, hipStream_t st) {
-  using G = StencilGeom<P, R, NW>;
+  using G = StencilGeom<P, R, NW, NBUF, WPC>;
   const size_t lds = G::lds_bytes(MASS);
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)stencil3d_kernel<P, R, NW, MASS>,
+    hipError_t e = hipFuncSetAttribute((const void *)stencil3d_kernel<P, R, NW, NBUF, WPC, MASS, CH>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -319,25 +424,37 @@ static hipError_t launch_stencil_t(const StencilArgs &a, hipStream_t st) {
   dim3 grid((a.Nx + G::TX - 1) / G::TX, (a.out_y1 - a.out_y0 + G::TY - 1) / G::TY,
             (a.out_z1 - a.out_z0 + a.zchunk - 1) / a.zchunk);
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return hipSuccess;
-  hipLaunchKernelGGL((stencil3d_kernel<P, R, NW, MASS>), grid, dim3(G::NT), lds, st, a);
+  hipLaunchKernelGGL((stencil3d_kernel<P, R, NW, NBUF, WPC, MASS, CH>), grid, dim3(G::NT), lds, st, a);
   return hipGetLastError();
+}
+
+template <int P, int R, int NW, int NBUF, int WPC>
+static hipError_t launch_stencil_p(bool mass, const StencilArgs &a, hipStream_t st) {
+  // 16-B LDS-DMA chunks need every staged row to start 16-B aligned
+  const bool vec = (a.Nx % 2 == 0) && ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0);
+  if (vec)
+    return mass ? launch_stencil_t<P, R, NW, NBUF, WPC, true, 16>(a, st)
+                : launch_stencil_t<P, R, NW, NBUF, WPC, false, 16>(a, st);
+  return mass ? launch_stencil_t<P, R, NW, NBUF, WPC, true, 4>(a, st)
+              : launch_stencil_t<P, R, NW, NBUF, WPC, false, 4>(a, st);
 }
 
 }  // namespace gdmk
 
+
+extern "C" int gdmk_stencil_tile_rows(int p) { return 16; }
+
 extern "C" hipError_t gdmk_launch_stencil(int p, bool mass, const gdmk::StencilArgs &a, hipStream_t st) {
   using namespace gdmk;
-  switch (p) {
-    case 1: return mass ? launch_stencil_t<1, 4, 8, true>(a, st) : launch_stencil_t<1, 4, 8, false>(a, st);
-    case 3: return mass ? launch_stencil_t<3, 4, 8, true>(a, st) : launch_stencil_t<3, 4, 8, false>(a, st);
-    case 5: return mass ? launch_stencil_t<5, 4, 8, true>(a, st) : launch_stencil_t<5, 4, 8, false>(a, st);
-    case 7: return mass ? launch_stencil_t<7, 4, 8, true>(a, st) : launch_stencil_t<7, 4, 8, false>(a, st);
-    case 9: return mass ? launch_stencil_t<9, 2, 8, true>(a, st) : launch_stencil_t<9, 2, 8, false>(a, st);
+  switch (p) {  // <P, R, NW, NBUF, WG per CU>
+    case 1: return launch_stencil_p<1, 2, 8, 3, 2>(mass, a, st);
+    case 3: return launch_stencil_p<3, 2, 8, 3, 2>(mass, a, st);
+    case 5: return launch_stencil_p<5, 2, 8, 3, 2>(mass, a, st);
+    case 7: return launch_stencil_p<7, 2, 8, 2, 2>(mass, a, st);
+    case 9: return launch_stencil_p<9, 2, 8, 2, 1>(mass, a, st);
     default: return hipErrorInvalidValue;
   }
 }
-
-extern "C" int gdmk_stencil_tile_rows(int p) { return p == 9 ? 16 : 32; }
 
 extern "C" hipError_t gdmk_launch_chol_lines(int p, double *v, int len, int64_t stride, int64_t n_lines, int64_t A,
                                              int64_t B, int64_t C, const double *lrow, const double *inv_diag,
