@@ -101,7 +101,7 @@ def pmc_traffic(args):
         vals = []
         for f in files:
             for row in csv.DictReader(open(f)):
-                if "stencil3d_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                if "stencil" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
                     vals.append(float(row["Counter_Value"]))
         shutil.rmtree(out, ignore_errors=True)
         if not vals:
@@ -226,7 +226,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "stencil3d_kernel<%d> (fused Kronecker stencil)" % p,
+            "kernel": "stencil7_kernel<p=%d> (fused Kronecker stencil)" % p,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/gdm_hip.h"
+#include "gdm_coeffs.h"
 #include "gdm_kernels.h"
 #include "gdm_setup.h"
 
@@ -82,9 +83,12 @@ struct gdm_op {
   double a[3] = {0, 0, 0};
   double nitsche = 0.0;
   // device tables
-  double *tMx = nullptr, *tBx = nullptr, *corrX = nullptr;
-  int x_corr_left = 0, x_corr_right = 0;
-  double *colMy = nullptr, *colBy = nullptr, *colMz = nullptr, *colBz = nullptr;
+  // stencil tables (kernel axes) and the scalars of the compile-time bands
+  double *corrX = nullptr, *yT1 = nullptr, *yT3 = nullptr, *zt = nullptr;
+  int x_corr_left = 0, x_corr_right = 0, x_toep = 0, y_toep = 0, z_toep = 0;
+  double sx = 0, cy[19] = {0};
+  // the same for the mass operator of an advection/wave op (gdm_mass_apply)
+  double *m_corrX = nullptr, *m_zt = nullptr;
   double *lrow[3] = {nullptr, nullptr, nullptr}, *invd[3] = {nullptr, nullptr, nullptr};
   std::vector<Face> faces;
   double *face_tmp = nullptr;
@@ -123,6 +127,25 @@ std::vector<double> band_cols(const gdm::Band &A, int pad, int pad_back) {
   for (int s = 0; s < n; ++s)
     for (int k = 0; k < W; ++k) t[(size_t)(s + pad) * W + k] = A(s - hb + k, s);
   return t;
+}
+
+// interior (Toeplitz) band of the unit-h 1D matrices: which 0 = M, 1 = C, 2 = L
+// -- exactly the compile-time constants the kernels use (gdm_coeffs.h)
+template <int P>
+std::vector<double> interior_band_t(int which) {
+  using IR = gdmk::InteriorRows<P>;
+  const double *src = which == 0 ? IR::m : (which == 1 ? IR::c : IR::l);
+  return std::vector<double>(src, src + 2 * P + 1);
+}
+
+std::vector<double> interior_band(int p, int which) {
+  switch (p) {
+    case 1: return interior_band_t<1>(which);
+    case 3: return interior_band_t<3>(which);
+    case 5: return interior_band_t<5>(which);
+    case 7: return interior_band_t<7>(which);
+    default: return interior_band_t<9>(which);
+  }
 }
 
 gdm::Band identity_band(int p) {
@@ -197,40 +220,83 @@ void build_tables(gdm_op *op) {
     }
     B[ax] = b;
   }
-  // x: wave-uniform Toeplitz row + corrections of the p+1 wall columns on
-  // each side (rows x <= p and x >= n - p involve the one-sided categories)
-  {
-    const int n = M[0].n, W = 2 * p + 1;
-    std::vector<double> tM(W, 0.0), tB(W, 0.0);
-    const bool has_interior = n >= 2 * p + 3;
-    if (has_interior) {
-      const int xi = n / 2;
-      for (int k = 0; k < W; ++k) {
-        tM[k] = M[0](xi, xi - p + k);
-        tB[k] = B[0](xi, xi - p + k);
-      }
-    }
-    op->x_corr_left = std::min(p + 1, n);
+  // Kernel tables.  Interior rows use the compile-time bands (gdm_coeffs.h):
+  // M = h mhat, B = beta bhat with bhat = chat (advection, convective) or
+  // lhat (wave) and beta = a_d resp. -1/h_d; see StencilArgs for the scalings.
+  const int W = 2 * p + 1;
+  double h[3], beta[3];
+  for (int ax = 0; ax < 3; ++ax) {
+    const int d = op->kdir[ax];
+    h[ax] = d < 0 ? 1.0 : (op->mesh.hi[d] - op->mesh.lo[d]) / op->mesh.n_subdivisions[d];
+    beta[ax] = 0.0;
+    if (d >= 0 && (op->kind == GDM_OP_ADVECTION || op->kind == GDM_OP_CONVECTIVE)) beta[ax] = op->a[d];
+    if (d >= 0 && op->kind == GDM_OP_WAVE) beta[ax] = -1.0 / h[ax];
+  }
+  auto toep = [&](int ax) { return op->K[ax] >= 2 * p + 3 ? 1 : 0; };
+  op->x_toep = toep(0);
+  op->y_toep = toep(1);
+  op->z_toep = toep(2);
+  const std::vector<double> mhat = interior_band(p, 0), bhat = interior_band(p, op->kind == GDM_OP_WAVE ? 2 : 1);
+  // x wall-column corrections (rows x <= p and x >= n - p use one-sided categories)
+  auto corr_table = [&](const gdm::Band &Mx, const gdm::Band &Bx, int &left, int &right) {
+    const int n = Mx.n;
+    left = std::min(p + 1, n);
     const int right_begin = std::max(p + 1, n - p - 1);
-    op->x_corr_right = std::max(0, n - right_begin);
+    right = std::max(0, n - right_begin);
     std::vector<double> corr((size_t)2 * (p + 1) * 2 * W, 0.0);
     auto fill = [&](int slot, int x) {
       for (int k = 0; k < W; ++k) {
-        corr[(size_t)slot * 2 * W + k] = M[0](x, x - p + k) - tM[k];
-        corr[(size_t)slot * 2 * W + W + k] = B[0](x, x - p + k) - tB[k];
+        const double tm = op->x_toep ? h[0] * mhat[k] : 0.0, tb = op->x_toep ? beta[0] * bhat[k] : 0.0;
+        corr[(size_t)slot * 2 * W + k] = (Mx(x, x - p + k) - tm) / h[0];
+        corr[(size_t)slot * 2 * W + W + k] = h[1] * (Bx(x, x - p + k) - tb);
       }
     };
-    for (int x = 0; x < op->x_corr_left; ++x) fill(x, x);
-    for (int j = 0; j < op->x_corr_right; ++j) fill(p + 1 + j, right_begin + j);
-    op->tMx = keep(op, dev_upload(tM));
-    op->tBx = keep(op, dev_upload(tB));
-    op->corrX = keep(op, dev_upload(corr));
-  }
+    for (int x = 0; x < left; ++x) fill(x, x);
+    for (int j = 0; j < right; ++j) fill(p + 1 + j, right_begin + j);
+    return corr;
+  };
+  auto scaled = [](const gdm::Band &A, double f) {
+    gdm::Band b = A;
+    for (double &v : b.a) v *= f;
+    return b;
+  };
+  // z column table: rows 0..2p = planes 0..2p, rows 2p+1..4p+1 = planes
+  // Nz-2p-1..Nz-1, row 4p+2 = the interior column; (e, d) pairs per entry
+  auto z_table = [&](const gdm::Band *Ez, const gdm::Band &Dz, double e_int, double d_int, const std::vector<double> &dhat) {
+    const int Nz = Dz.n;
+    std::vector<double> t((size_t)(2 * W + 1) * W * 2, 0.0);
+    auto col = [&](int row, int zz) {
+      if (zz < 0 || zz >= Nz) return;
+      for (int k = 0; k < W; ++k) {
+        const int zr = zz - p + k;
+        t[((size_t)row * W + k) * 2 + 0] = Ez ? (*Ez)(zr, zz) : 0.0;
+        t[((size_t)row * W + k) * 2 + 1] = Dz(zr, zz);
+      }
+    };
+    for (int r = 0; r < W; ++r) col(r, r);
+    for (int r = 0; r < W; ++r) col(W + r, Nz - W + r);
+    for (int k = 0; k < W; ++k) {
+      t[((size_t)2 * W * W + k) * 2 + 0] = Ez ? e_int * mhat[2 * p - k] : 0.0;
+      t[((size_t)2 * W * W + k) * 2 + 1] = d_int * dhat[2 * p - k];
+    }
+    return t;
+  };
   const int ypad = p + 64;  // >= p + max tile rows
-  op->colMy = keep(op, dev_upload(band_cols(M[1], p, ypad)));
-  op->colBy = keep(op, dev_upload(band_cols(B[1], p, ypad)));
-  op->colMz = keep(op, dev_upload(band_cols(M[2], 0, 0)));
-  op->colBz = keep(op, dev_upload(band_cols(B[2], 0, 0)));
+  const bool mass = op->kind == GDM_OP_MASS;
+  const gdm::Band Bz = scaled(B[2], h[0] * h[1]), Mz = scaled(M[2], h[0] * h[1]);
+  op->corrX = keep(op, dev_upload(corr_table(M[0], B[0], op->x_corr_left, op->x_corr_right)));
+  op->yT1 = keep(op, dev_upload(band_cols(scaled(M[1], 1.0 / h[1]), p, ypad)));
+  op->yT3 = keep(op, dev_upload(band_cols(scaled(B[1], h[0]), p, ypad)));
+  op->m_zt = keep(op, dev_upload(z_table(nullptr, Mz, 0.0, h[0] * h[1] * h[2], mhat)));
+  op->zt = mass ? op->m_zt : keep(op, dev_upload(z_table(&M[2], Bz, h[2], beta[2] * h[0] * h[1], bhat)));
+  op->sx = h[1] * beta[0];
+  for (int k = 0; k < W; ++k) op->cy[k] = h[0] * beta[1] * bhat[k];
+  // mass operator tables for gdm_mass_apply on a non-mass op
+  {
+    gdm::Band zero0(M[0].n, p);
+    int l = 0, r = 0;
+    op->m_corrX = keep(op, dev_upload(corr_table(M[0], zero0, l, r)));
+  }
   // banded Cholesky factors of the 1D mass matrices (exact Kronecker inverse)
   for (int ax = 0; ax < 3; ++ax) {
     if (op->K[ax] <= 1) continue;
@@ -363,17 +429,30 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst)
     a.out_z0 = 0; a.out_z1 = 1; a.out_y0 = L.owned_plane_begin; a.out_y1 = L.owned_plane_end;
   }
   a.zchunk = std::max(1, std::min(op->zchunk, a.out_z1 - a.out_z0));
-  a.tMx = op->tMx;
-  a.tBx = op->tBx;
-  a.corrX = op->corrX;
+  a.x_toep = op->x_toep;
+  a.y_toep = op->y_toep;
+  a.z_toep = op->z_toep;
   a.x_corr_left = op->x_corr_left;
   a.x_corr_right = op->x_corr_right;
-  a.colMy = op->colMy;
-  a.colBy = op->colBy;
-  a.colMz = op->colMz;
-  a.colBz = op->colBz;
+  const bool as_mass = mass || op->kind == GDM_OP_MASS;
+  a.yT1 = op->yT1;
+  a.yT3 = op->yT3;
+  if (as_mass) {
+    a.sx = 0.0;
+    a.corrX = op->m_corrX;
+    a.zt = op->m_zt;
+  } else {
+    a.sx = op->sx;
+    for (int k = 0; k < 19; ++k) a.cy[k] = op->cy[k];
+    a.corrX = op->corrX;
+    a.zt = op->zt;
+  }
+#ifdef GDM_DIAG
+  if (const char *env = std::getenv("GDM_DBG")) a.dbg = std::atoi(env);
+#endif
   if (L.n_owned == 0) return hipSuccess;
-  return gdmk_launch_stencil(op->p, mass, a, op->stream);
+  const int bk = as_mass ? 0 : (op->kind == GDM_OP_WAVE ? 2 : 1);
+  return gdmk_launch_stencil(op->p, bk, a, op->stream);
 }
 
 void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned) {
@@ -413,8 +492,8 @@ int choose_zchunk(const gdm_op *op) {
   const int nz = op->part_axis == 2 ? (op->layout.owned_plane_end - op->layout.owned_plane_begin) : 1;
   const int ty = gdmk_stencil_tile_rows(op->p);
   const int64_t tiles = (int64_t)((op->K[0] + 63) / 64) * ((op->K[1] + ty - 1) / ty);
-  // aim for ~512 workgroups (2 rounds of one 8-wave workgroup per CU)
-  const int64_t chunks = std::max<int64_t>(1, (512 + tiles - 1) / tiles);
+  // aim for one round of ~256 workgroups (one 16-wave workgroup per CU)
+  const int64_t chunks = std::max<int64_t>(1, (256 + tiles - 1) / tiles);
   int zc = (int)std::max<int64_t>(8, (nz + chunks - 1) / chunks);
   return std::max(1, zc);
 }

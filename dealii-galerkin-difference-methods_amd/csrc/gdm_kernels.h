@@ -8,6 +8,14 @@ namespace gdmk {
 // Fused Kronecker stencil: out = B_x M_y M_z + M_x B_y M_z + M_x M_y B_z (or
 // M_x M_y M_z for the mass operator) applied to the input box, written for
 // the output box.  Arrays are [z - z0][y - y0][x] with full x extent.
+//
+// Interior x and y rows use the compile-time unit bands mhat, bhat of
+// gdm_coeffs.h (bhat = chat for advection/convective, lhat for wave):
+//   A' = M_x u / h_x = mhat*u,   B* = h_y B_x u = sx bhat*u,
+//   D' = M_y A' / h_y,           E  = M_y B* / h_y + h_x B_y A' = mhat*B* + cy*A'
+//   out(z') += M_z(z', z) E(z) + h_x h_y B_z(z', z) D'(z)   (mass: h_x h_y M_z D')
+// x/y rows next to a wall read runtime tables; z columns come from a small
+// column table (wall columns + the interior column).
 struct StencilArgs {
   const double *__restrict__ src;
   double *__restrict__ dst;
@@ -15,16 +23,22 @@ struct StencilArgs {
   int in_y0, in_y1, in_z0, in_z1;      // valid input box (global indices)
   int out_y0, out_y1, out_z0, out_z1;  // output box
   int zchunk;                          // output planes per workgroup
-  const double *__restrict__ tMx;      // [2p+1] Toeplitz (interior) row of M_x
-  const double *__restrict__ tBx;      // [2p+1] Toeplitz (interior) row of B_x
-  const double *__restrict__ corrX;    // [2(p+1)][2 (2p+1)] (row_M(x) - tM, row_B(x) - tB) of the wall
-                                       //   columns: slot x for x < x_corr_left, slot p+1+j for
-                                       //   column Nx - x_corr_right + j
-  int x_corr_left, x_corr_right;       // wall columns with corrections (<= p+1 each)
-  const double *__restrict__ colMy;    // [Ny + 2p][2p+1] row s + p: M_y(s - p + k, s)
-  const double *__restrict__ colBy;
-  const double *__restrict__ colMz;    // [Nz][2p+1]      M_z(z - p + k, z)
-  const double *__restrict__ colBz;
+  // Toeplitz interiors exist (N >= 2p + 3) per axis
+  int x_toep, y_toep, z_toep;
+  double sx;        // h_y beta_x
+  double cy[19];    // h_x beta_y bhat[k]
+  // x: wall-column corrections [2(p+1)][2(2p+1)]: ((M_x row - [x_toep] h_x mhat) / h_x,
+  //    h_y (B_x row - [x_toep] beta_x bhat)); slot x for x < x_corr_left, slot p+1+j
+  //    for column Nx - x_corr_right + j
+  const double *__restrict__ corrX;
+  int x_corr_left, x_corr_right;
+  // y wall rows, column tables [Ny + 2p + pad][2p+1] (row s + p: A(s - p + k, s)):
+  const double *__restrict__ yT1;  // M_y / h_y
+  const double *__restrict__ yT3;  // h_x B_y
+  // z columns [2(2p+1)+1][2p+1][2] = (e, d) pairs, out(zz - p + k) += e E + d D':
+  // rows 0..2p: planes 0..2p; rows 2p+1..4p+1: planes Nz-2p-1..Nz-1; row 4p+2: interior
+  const double *__restrict__ zt;
+  int dbg;  // diagnostic builds only (-DGDM_DIAG): bits disable kernel phases
 };
 
 // Inflow boundary-data projection of one box face (two tangential directions
@@ -45,7 +59,7 @@ struct FaceArgs {
 }  // namespace gdmk
 
 extern "C" {
-hipError_t gdmk_launch_stencil(int p, bool mass, const gdmk::StencilArgs &a, hipStream_t st);
+hipError_t gdmk_launch_stencil(int p, int bk, const gdmk::StencilArgs &a, hipStream_t st);
 int gdmk_stencil_tile_rows(int p);
 hipError_t gdmk_launch_chol_lines(int p, double *v, int len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,
                                   int64_t C, const double *lrow, const double *inv_diag, hipStream_t st);

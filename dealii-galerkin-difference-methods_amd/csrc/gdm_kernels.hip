@@ -21,73 +21,19 @@
 #include <stdint.h>
 #include <cstdlib>
 
+#include "gdm_coeffs.h"
 #include "gdm_kernels.h"
 
 namespace gdmk {
 
 
 
-template <int P, int R, int NW, int NBUF_ = 3, int WPC_ = 2>
-struct StencilGeom {
-  static constexpr int W = 2 * P + 1;      // band width = ring size
-  static constexpr int TX = 64;            // one wave row
-  static constexpr int TY = R * NW;        // output rows per tile
-  static constexpr int UR = TY + 2 * P;    // staged rows
-  static constexpr int XH = (P + 1) & ~1;  // x halo, even -> 16-B aligned row start
-  static constexpr int RL = TX + 2 * XH;   // staged row length (doubles)
-  static constexpr int NT = 64 * NW;
-  static constexpr int NBUF = NBUF_;       // plane ring: current + NBUF-1 in flight
-  static constexpr int WPC = WPC_;         // resident workgroups per CU (register budget)
-  static constexpr int NCORR = 2 * (P + 1);  // x columns whose band row differs from the Toeplitz row
-  static constexpr int USZ = UR * RL;      // doubles per staged plane
-  static constexpr size_t lds_bytes(bool mass) {
-    return sizeof(double) * ((size_t)NBUF * USZ + (size_t)UR * TX * (mass ? 1 : 2) + (size_t)NCORR * 2 * W);
-  }
-};
-
-// Stage one plane tile (rows y0-P .. y0+TY+P-1, columns x0-XH .. x0+TX+XH-1)
-// into LDS with LDS-DMA (buffer_load ... lds).  Chunks outside the valid
-// input box get an out-of-range voffset, which the buffer range check turns
-// into zeros.  CH = 16 (2 doubles per lane; rows 16-B aligned: Nx even) or
-// CH = 4 (any Nx).
-template <int P, int R, int NW, int CH>
-struct StageCount {
-  using G = StencilGeom<P, R, NW>;
-  static constexpr int DPC = CH / 4;                 // dwords per chunk
-  static constexpr int CPR = G::RL * 2 / DPC;        // chunks per row
-  static constexpr int NCH = G::UR * CPR;            // chunks per plane
-  static constexpr int NI = (NCH + 63) / 64;         // wave-instructions per plane
-  static constexpr int MIN_PER_WAVE = NI / NW;       // issued by every wave
-};
-
-template <int P, int R, int NW, int CH>
-__device__ __forceinline__ void stage_plane(const StencilArgs &a, int zz, int x0, int y0, double *ubuf, int wv,
-                                            int lane) {
-  using G = StencilGeom<P, R, NW>;
-  using SC = StageCount<P, R, NW, CH>;
-  const int ny_in = a.in_y1 - a.in_y0;
-  const double *plane = a.src + (int64_t)(zz - a.in_z0) * ny_in * a.Nx;
-  const int nbytes = (int)((int64_t)ny_in * a.Nx * 8);
-  __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)plane, 0, nbytes, 0x00020000);
-  for (int j = wv; j < SC::NI; j += NW) {
-    const int e = j * 64 + lane;
-    const int r = e / SC::CPR, c = e - r * SC::CPR;
-    const int gy = y0 - P + r;
-    const int gx2 = (x0 - G::XH) * 2 + c * SC::DPC;  // dword column
-    uint32_t voff = 0x80000000u;                      // out of range -> zeros
-    if (e < SC::NCH && gy >= a.in_y0 && gy < a.in_y1 && gx2 >= 0 && gx2 < 2 * a.Nx)
-      voff = (uint32_t)(((int64_t)(gy - a.in_y0) * a.Nx * 2 + gx2) * 4);
-    if (e < SC::NCH) {
-      auto *dst = (__attribute__((address_space(3))) void *)((char *)ubuf + (size_t)j * 64 * CH);
-      if constexpr (CH == 16)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, voff, 0, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, voff, 0, 0, 0);
-    }
-  }
-}
-
 #define GDM_WAIT_VMCNT(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
+#ifdef GDM_DIAG
+#define GDM_DBG(a, bit) (((a).dbg & (bit)) != 0)
+#else
+#define GDM_DBG(a, bit) false
+#endif
 #define GDM_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
 // Coefficient tables are read-only for the whole launch and indexed by
@@ -96,177 +42,456 @@ __device__ __forceinline__ void stage_plane(const StencilArgs &a, int zz, int x0
 typedef __attribute__((address_space(4))) const double cdouble;
 __device__ __forceinline__ cdouble *cptr(const double *p) { return (cdouble *)(p); }
 
-// Per-workgroup state of the z-march (all wave-uniform except lane/x).
-struct MarchCtx {
-  double *ubase, *as, *bs, *corr;
-  int lane, wv, x0, y0, x, zc0, zc1, zs, ze, zend, ybase, cslot, ny_out;
-  bool need_corr;
+// ===========================================================================
+// Fused Kronecker stencil, v7: producer / consumer waves.
+//
+// A workgroup owns a 64 x TY column of (x, y) and marches it along z.
+//   * NP producer waves stage the (TY + 2p) x (64 + 2p) input plane tile into
+//     LDS by LDS-DMA (buffer_load ... lds, out-of-box rows/columns read as 0)
+//     and run the x-sweep, 4 consecutive x per lane from a 16-B aligned
+//     register window (ds_read_b128).  Each producer wave DMAs exactly the
+//     row groups it sweeps, so the u ring needs no workgroup barrier: a
+//     counted vmcnt per wave keeps one plane of DMA in flight.
+//   * NC consumer waves (lane = x, R rows each) run the y-sweep from the A/B
+//     planes and scatter into a register ring of 2p+1 output planes, retiring
+//     one finished plane per input plane with coalesced row stores.
+// The two roles hand over one A/B plane per barrier (double-buffered), so a
+// wave holds either the x-sweep temporaries or the ring, never both.
+// ===========================================================================
+template <int P, int R, int NC, int NP, int BK>
+struct Geom7 {
+  static constexpr int W = 2 * P + 1;
+  static constexpr int TX = 64;
+  static constexpr int TY = R * NC;
+  static constexpr int UR = TY + 2 * P;
+  static constexpr int XH = P + 1;  // even: keeps the x windows 16-B aligned
+  static constexpr int RL0 = TX + 2 * XH;
+  // row pitch = 2 mod 4 doubles: the two rows a ds_read_b128 lane group spans
+  // land on disjoint bank halves
+  static constexpr int RL = (RL0 % 4 == 2) ? RL0 : RL0 + 2;
+  static constexpr int NW = NP + NC;
+  static constexpr int NT = 64 * NW;
+  static constexpr int NG = (UR + 3) / 4;  // producer row groups (4 rows = one wave pass)
+  static constexpr int NPASS = (NG + NP - 1) / NP;
+  static constexpr int USZ = NG * 4 * RL;
+  static constexpr int NAB = BK == 0 ? 1 : 2;
+  static constexpr int ABSZ = NAB * UR * TX;
+  static constexpr int NZR = 2 * W + 1;
+  static constexpr int ZTSZ = NZR * W * 2;
+  static constexpr int NCORR = 2 * (P + 1);
+  static constexpr int CORRSZ = NCORR * 2 * W;
+  static constexpr int YCSZ = UR * W * 2;  // y-wall columns of the tile rows, (M_y/h_y, h_x B_y) pairs
+  static constexpr int NWIN = 2 * P + 6;
+  static constexpr int OFF_AB = 2 * USZ;
+  static constexpr int OFF_ZT = OFF_AB + 2 * ABSZ;
+  static constexpr int OFF_YC = OFF_ZT + ZTSZ;
+  static constexpr int OFF_CORR = OFF_YC + YCSZ;
+  static constexpr size_t lds_bytes() { return sizeof(double) * (size_t)(OFF_CORR + CORRSZ); }
 };
 
-// One input plane zz at ring phase JP (= zz mod W): stage/sweep/scatter, then
-// retire output plane zz - p.  JP is a template parameter so every ring slot
-// index is a compile-time constant and the ring stays in registers.
-template <int JP, int P, int R, int NW, int NBUF, int WPC, bool MASS, int CH>
-__device__ __forceinline__ void march_plane(const StencilArgs &a, const MarchCtx &c, double (&acc)[2 * P + 1][R],
-                                            int zz) {
-  using G = StencilGeom<P, R, NW, NBUF, WPC>;
-  using SC = StageCount<P, R, NW, CH>;
-  constexpr int W = G::W, TX = G::TX, UR = G::UR, RL = G::RL, XH = G::XH, USZ = G::USZ;
-  if (zz < c.ze) {
-    // ---- 1. this wave's DMA of plane zz landed; barrier: every wave's did
-    //         and every wave finished plane zz-1 ----
-    if (zz + 1 < c.ze)
-      GDM_WAIT_VMCNT(SC::MIN_PER_WAVE);
-    else
-      GDM_WAIT_VMCNT(0);
-    GDM_LDS_BARRIER();
-    // buffer (zz+NBUF-1) % NBUF == (zz-1) % NBUF was last read by the x-sweep of zz-1
-    if (zz + NBUF - 1 < c.ze)
-      stage_plane<P, R, NW, CH>(a, zz + NBUF - 1, c.x0, c.y0, c.ubase + ((zz + NBUF - 1) % NBUF) * USZ, c.wv,
-                                c.lane);
-    const double *us = c.ubase + (zz % NBUF) * USZ;
-    // ---- 2. x-sweep: A = M_x u, Bv = B_x u on the UR staged rows ----
-    // (the Toeplitz row is re-read from the scalar cache every plane instead
-    //  of pinning 4(2p+1) SGPRs for the whole kernel)
-    cdouble *tM = cptr(a.tMx), *tB = cptr(a.tBx);
-    asm volatile("" : "+s"(tM), "+s"(tB));
-    for (int r = c.wv; r < UR; r += NW) {
-      const double *ur = us + r * RL + c.lane + (XH - P);
-      double uk[W];
-#pragma unroll
-      for (int k = 0; k < W; ++k) uk[k] = ur[k];
-      double am = 0.0, ab = 0.0;
-#pragma unroll
-      for (int k = 0; k < W; ++k) {
-        am = fma(tM[k], uk[k], am);
-        if (!MASS) ab = fma(tB[k], uk[k], ab);
-      }
-      if (c.need_corr && c.cslot >= 0) {
-        const double *cm = c.corr + c.cslot * 2 * W;
-#pragma unroll
-        for (int k = 0; k < W; ++k) {
-          am = fma(cm[k], uk[k], am);
-          if (!MASS) ab = fma(cm[W + k], uk[k], ab);
-        }
-      }
-      c.as[r * TX + c.lane] = am;
-      if (!MASS) c.bs[r * TX + c.lane] = ab;
+template <int P, int R, int NC, int NP, int BK, int CH>
+struct Dma7 {
+  using G = Geom7<P, R, NC, NP, BK>;
+  static constexpr int DPC = CH / 4;             // dwords per lane
+  static constexpr int CPR = G::RL * 2 / DPC;    // lane chunks per LDS row
+  static constexpr int ROWS_LAST = G::UR - 4 * (G::NG - 1);
+  static constexpr int NI_FULL = (4 * CPR + 63) / 64;
+  static constexpr int NI_LAST = (ROWS_LAST * CPR + 63) / 64;
+  static constexpr int ni(int g) { return g == G::NG - 1 ? NI_LAST : NI_FULL; }
+  // DMA instructions producer wave w issues per plane
+  static constexpr int nd(int w) {
+    int s = 0;
+    for (int ps = 0; ps < G::NPASS; ++ps)
+      if (w + ps * NP < G::NG) s += ni(w + ps * NP);
+    return s;
+  }
+};
+
+typedef __attribute__((address_space(3))) double ldouble;
+typedef double dpair __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) dpair ldouble2;
+typedef __attribute__((address_space(3))) const double lcdouble;
+typedef __attribute__((address_space(3))) const dpair lcdouble2;
+// compiler-only fence: no memory access and no instruction crosses it, so the
+// scheduler cannot hoist all LDS reads of a sweep to its top (their registers
+// would overlap the accumulator ring)
+#define GDM_FENCE()                      \
+  do {                                   \
+    asm volatile("" ::: "memory");       \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+
+struct Tile7 {
+  ldouble *u0, *ab0, *zt, *yc, *corr;
+  int lane, wv, x0, y0, zc0, zc1, zs, ze, zend;
+  // x wall columns inside this tile: nl from the left wall, nr from column rs on
+  int nl, rs, ncw;
+};
+
+// wait until at most nd(wv) DMA instructions of this producer wave are in flight
+template <int I, int P, int R, int NC, int NP, int BK, int CH>
+__device__ __forceinline__ void wait_dma_plane(int wv) {
+  if constexpr (I < NP) {
+    if (wv == I) {
+      GDM_WAIT_VMCNT((Dma7<P, R, NC, NP, BK, CH>::nd(I)));
+      return;
     }
-    GDM_LDS_BARRIER();
-    // ---- 3. y-sweep: scatter the R + 2p staged rows into this wave's R rows ----
-    double D[R], E[R];
+    wait_dma_plane<I + 1, P, R, NC, NP, BK, CH>(wv);
+  }
+}
+
+// LDS-DMA of row group g of plane zz into u slot ubuf
+template <int P, int R, int NC, int NP, int BK, int CH>
+__device__ __forceinline__ void stage_group7(const StencilArgs &a, const Tile7 &t, int zz, int g, ldouble *ubuf) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  using S = Dma7<P, R, NC, NP, BK, CH>;
+  const int ny_in = a.in_y1 - a.in_y0;
+  const double *plane = a.src + (int64_t)(zz - a.in_z0) * ny_in * a.Nx;
+  const int nbytes = (int)((int64_t)ny_in * a.Nx * 8);
+  __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)plane, 0, nbytes, 0x00020000);
+  const bool last = g == G::NG - 1;
+  const int nch = (last ? S::ROWS_LAST : 4) * S::CPR;
+  const int ni = last ? S::NI_LAST : S::NI_FULL;
+  auto *gbase = (__attribute__((address_space(3))) char *)(ubuf + g * 4 * G::RL);
 #pragma unroll
-    for (int j = 0; j < R; ++j) D[j] = E[j] = 0.0;
-#pragma unroll
-    for (int t = 0; t < R + 2 * P; ++t) {
-      const int trow = c.wv * R + t;  // tile row
-      const int s = c.ybase - P + t;  // global row, in [-P, Ny + P + TY)
-      const double av = c.as[trow * TX + c.lane];
-      const double bv = MASS ? 0.0 : c.bs[trow * TX + c.lane];
-      cdouble *cm = cptr(a.colMy) + (size_t)(s + P) * W;
-      cdouble *cb = cptr(a.colBy) + (size_t)(s + P) * W;
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const int k = j + 2 * P - t;
-        if (k >= 0 && k < W) {
-          const double m = cm[k];
-          D[j] = fma(m, av, D[j]);
-          if (!MASS) E[j] = fma(m, bv, fma(cb[k], av, E[j]));
-        }
-      }
-    }
-    // ---- 4. z-scatter into the register ring ----
-    cdouble *cmz = cptr(a.colMz) + (size_t)zz * W;
-    cdouble *cbz = cptr(a.colBz) + (size_t)zz * W;
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      constexpr int base = JP - P + 2 * W;
-      const int slot = (base + k) % W;
-      const double m = cmz[k];
-      if (MASS) {
-#pragma unroll
-        for (int j = 0; j < R; ++j) acc[slot][j] = fma(m, D[j], acc[slot][j]);
-      } else {
-        const double b = cbz[k];
-#pragma unroll
-        for (int j = 0; j < R; ++j) acc[slot][j] = fma(m, E[j], fma(b, D[j], acc[slot][j]));
+  for (int i = 0; i < S::NI_FULL; ++i) {
+    if (i < ni) {
+      const int e = i * 64 + t.lane;
+      const int rr = e / S::CPR, c = e - rr * S::CPR;
+      const int gy = t.y0 - P + 4 * g + rr;
+      const int gx2 = (t.x0 - G::XH) * 2 + c * S::DPC;  // dword column
+      uint32_t voff = 0x80000000u;                      // out of range -> zeros
+      if (e < nch && gy >= a.in_y0 && gy < a.in_y1 && gx2 >= 0 && gx2 < 2 * a.Nx)
+        voff = (uint32_t)(((int64_t)(gy - a.in_y0) * a.Nx * 2 + gx2) * 4);
+      if (e < nch) {
+        auto *dst = (__attribute__((address_space(3))) void *)(gbase + i * 64 * CH);
+        if constexpr (CH == 16)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, voff, 0, 0, 0);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, voff, 0, 0, 0);
       }
     }
   }
-  // ---- retire output plane zz - p (complete: every contributing plane done) ----
+}
+
+template <int P, int R, int NC, int NP, int BK, int CH>
+__device__ __forceinline__ void stage_plane7(const StencilArgs &a, const Tile7 &t, int zz, ldouble *ubuf) {
+  using G = Geom7<P, R, NC, NP, BK>;
+#pragma unroll
+  for (int ps = 0; ps < G::NPASS; ++ps) {
+    const int g = t.wv + ps * NP;
+    if (g < G::NG) stage_group7<P, R, NC, NP, BK, CH>(a, t, zz, g, ubuf);
+  }
+}
+
+// x-sweep of the row groups of this producer wave: A' = mhat*u, B* = sx bhat*u
+// (+ wall-column corrections), 4 consecutive x per lane.
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void xsweep7(const StencilArgs &a, const Tile7 &t, lcdouble *us, ldouble *ab) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  using IR = InteriorRows<P>;
+  constexpr int W = G::W, TX = G::TX, RL = G::RL;
+  ldouble *as = ab, *bs = ab + G::UR * TX;
+  const int rr = t.lane >> 4, q = t.lane & 15;
+#pragma unroll
+  for (int ps = 0; ps < G::NPASS; ++ps) {
+    const int g = t.wv + ps * NP;
+    if (g >= G::NG) break;
+    const int r = 4 * g + rr;
+    if (r < G::UR) {
+      double A[4], B[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) A[j] = B[j] = 0.0;
+      if (a.x_toep) {
+        lcdouble2 *wp = (lcdouble2 *)(us + r * RL + 4 * q);
+        double w[G::NWIN];
+#pragma unroll
+        for (int i = 0; i < G::NWIN / 2; ++i) {
+          const dpair v = wp[i];
+          w[2 * i] = v.x;
+          w[2 * i + 1] = v.y;
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            A[j] = fma(IR::m[k], w[j + k + 1], A[j]);
+            if constexpr (BK == 1) B[j] = fma(IR::c[k], w[j + k + 1], B[j]);
+            if constexpr (BK == 2) B[j] = fma(IR::l[k], w[j + k + 1], B[j]);
+          }
+      }
+      ldouble2 *ap = (ldouble2 *)(as + r * TX + 4 * q);
+      ap[0] = dpair{A[0], A[1]};
+      ap[1] = dpair{A[2], A[3]};
+      if constexpr (BK != 0) {
+        ldouble2 *bp = (ldouble2 *)(bs + r * TX + 4 * q);
+        bp[0] = dpair{a.sx * B[0], a.sx * B[1]};
+        bp[1] = dpair{a.sx * B[2], a.sx * B[3]};
+      }
+    }
+    // wall columns of this tile: add the (row - Toeplitz) corrections
+    if (t.ncw > 0) {
+      const int nrow = min(4, G::UR - 4 * g);
+      for (int e = t.lane; e < nrow * t.ncw; e += 64) {
+        const int r2 = 4 * g + e / t.ncw, idx = e % t.ncw;
+        const int x = idx < t.nl ? t.x0 + idx : t.rs + (idx - t.nl);
+        const int cs = x < a.x_corr_left ? x : (P + 1) + (x - (a.Nx - a.x_corr_right));
+        const int lx = x - t.x0;
+        lcdouble *ur = us + r2 * RL + lx + 1;  // tap k of column x
+        lcdouble *cm = t.corr + cs * 2 * W;
+        double dA = 0.0, dB = 0.0;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          const double uv = ur[k];
+          dA = fma(cm[k], uv, dA);
+          if constexpr (BK != 0) dB = fma(cm[W + k], uv, dB);
+        }
+        as[r2 * TX + lx] += dA;
+        if constexpr (BK != 0) bs[r2 * TX + lx] += dB;
+      }
+    }
+  }
+}
+
+// y-sweep of the consumer's R rows: D' (and E) from A/B set `ab`
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void ysweep7(const StencilArgs &a, const Tile7 &t, bool ytoep, int ybase,
+                                        lcdouble *ab, double (&D)[R], double (&E)[R]) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  using IR = InteriorRows<P>;
+  constexpr int W = G::W, TX = G::TX;
+  // volatile: one ds_read_b64 per row (the compiler would pair rows into
+  // ds_read2st64_b64, which runs at half the LDS rate)
+  const volatile lcdouble *as = ab + ((t.wv - NP) * R) * TX + t.lane;
+  const volatile lcdouble *bs = as + G::UR * TX;
+#pragma unroll
+  for (int j = 0; j < R; ++j) D[j] = E[j] = 0.0;
+  if (ytoep) {
+    // rows are read one pair ahead of their use
+    constexpr int NR = R + 2 * P;
+    double av[NR], bv[NR];
+    av[0] = as[0];
+    if constexpr (BK != 0) bv[0] = bs[0];
+    if constexpr (NR > 1) {
+      av[1] = as[TX];
+      if constexpr (BK != 0) bv[1] = bs[TX];
+    }
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      if (s % 2 == 0) {
+        GDM_FENCE();
+#pragma unroll
+        for (int u = s + 2; u < s + 4 && u < NR; ++u) {
+          av[u] = as[u * TX];
+          if constexpr (BK != 0) bv[u] = bs[u * TX];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int k = s - j;  // row form: M(y_j, y_j - p + k)
+        if (k >= 0 && k < W) {
+          D[j] = fma(IR::m[k], av[s], D[j]);
+          if constexpr (BK != 0) E[j] = fma(IR::m[k], bv[s], fma(a.cy[k], av[s], E[j]));
+        }
+      }
+    }
+  } else {
+    // rows next to a y wall: column coefficients from the tile's LDS table
+    // (broadcast reads), rows and pairs read one step ahead of their use
+    constexpr int NR = R + 2 * P;
+    lcdouble2 *yc = (lcdouble2 *)t.yc + ((t.wv - NP) * R) * W;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      GDM_FENCE();
+      const double av = as[s * TX];
+      const double bv = BK ? bs[s * TX] : 0.0;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int k = j + 2 * P - s;  // column form: M(s - p + k, s)
+        if (k >= 0 && k < W) {
+          const dpair c = yc[s * W + k];
+          D[j] = fma(c.x, av, D[j]);
+          if constexpr (BK != 0) E[j] = fma(c.x, bv, fma(c.y, av, E[j]));
+        }
+      }
+    }
+  }
+}
+
+// One consumer plane: input plane zz, JP = (zz - zs) mod W (compile-time ring
+// phase).  The z column comes from the LDS column table (wall columns, or the
+// shared interior column), read one (e, d) pair ahead of its use.
+template <int JP, int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void cplane7(const StencilArgs &a, const Tile7 &t, bool ytoep, int ybase, bool full,
+                                        double (&acc)[2 * P + 1][R], int zz) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  constexpr int W = G::W;
+  double D[R], E[R];
+  if (zz < t.ze) {
+    if (GDM_DBG(a, 1)) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) D[j] = E[j] = (double)zz;
+    } else {
+      ysweep7<P, R, NC, NP, BK>(a, t, ytoep, ybase, t.ab0 + ((zz - t.zs) & 1) * G::ABSZ, D, E);
+    }
+    if (!GDM_DBG(a, 16)) GDM_LDS_BARRIER();
+  } else {
+#pragma unroll
+    for (int j = 0; j < R; ++j) D[j] = E[j] = 0.0;
+  }
+  const int row = zz < W ? zz : (zz >= a.Nz - W && zz < a.Nz ? W + zz - (a.Nz - W) : 2 * W);
+  lcdouble2 *zc = (lcdouble2 *)t.zt + row * W;
+  dpair cur = zc[0];
+  if (!GDM_DBG(a, 2)) {
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    GDM_FENCE();
+    const dpair nxt = zc[k + 1 < W ? k + 1 : k];
+    const int slot = (JP - P + k + 2 * W) % W;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if constexpr (BK == 0)
+        acc[slot][j] = fma(cur.y, D[j], acc[slot][j]);
+      else
+        acc[slot][j] = fma(cur.x, E[j], fma(cur.y, D[j], acc[slot][j]));
+    }
+    cur = nxt;
+  }
+  }
+  // The ring values only feed the conditional retire stores; without this
+  // opaque use LLVM sinks each slot's whole FMA chain into its store branch
+  // and keeps every plane's D/E and coefficients alive until then.
+#pragma unroll
+  for (int s = 0; s < W; ++s)
+#pragma unroll
+    for (int j = 0; j < R; ++j) asm volatile("" : "+v"(acc[s][j]));
+  // retire output plane zz - p
   constexpr int rslot = (JP - P + 2 * W) % W;
   const int zo = zz - P;
-  if (zo >= c.zc0 && zo < c.zc1) {
-    const int Nx = a.Nx;
-    double *orow = a.dst + ((int64_t)(zo - a.out_z0) * c.ny_out + (c.ybase - a.out_y0)) * Nx + c.x;
+  if (zo >= t.zc0 && zo < t.zc1) {
+    const int Nx = a.Nx, x = t.x0 + t.lane;
+    double *orow = a.dst + ((int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) + (ybase - a.out_y0)) * Nx + x;
+    if (full) {
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-      if (c.x < Nx && c.ybase + j < a.out_y1) orow[(int64_t)j * Nx] = acc[rslot][j];
+      for (int j = 0; j < R; ++j) orow[(int64_t)j * Nx] = acc[rslot][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (x < Nx && ybase + j < a.out_y1) orow[(int64_t)j * Nx] = acc[rslot][j];
+    }
   }
 #pragma unroll
   for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
 }
 
-template <int JP, int P, int R, int NW, int NBUF, int WPC, bool MASS, int CH>
-__device__ __forceinline__ void march_phases(const StencilArgs &a, const MarchCtx &c, double (&acc)[2 * P + 1][R],
-                                             int zb) {
+template <int JP, int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void cblock7(const StencilArgs &a, const Tile7 &t, bool ytoep, int ybase, bool full,
+                                        double (&acc)[2 * P + 1][R], int zb) {
   if constexpr (JP < 2 * P + 1) {
-    const int zz = zb + JP;
-    if (zz >= c.zs && zz < c.zend) march_plane<JP, P, R, NW, NBUF, WPC, MASS, CH>(a, c, acc, zz);
-    march_phases<JP + 1, P, R, NW, NBUF, WPC, MASS, CH>(a, c, acc, zb);
+    cplane7<JP, P, R, NC, NP, BK>(a, t, ytoep, ybase, full, acc, zb + JP);
+    cblock7<JP + 1, P, R, NC, NP, BK>(a, t, ytoep, ybase, full, acc, zb);
   }
 }
 
-template <int P, int R, int NW, int NBUF, int WPC, bool MASS, int CH>
-__global__ void __launch_bounds__(64 * NW, (64 * NW * WPC) / 256) stencil3d_kernel(StencilArgs a) {
-  using G = StencilGeom<P, R, NW, NBUF, WPC>;
-  constexpr int W = G::W, TX = G::TX, UR = G::UR, USZ = G::USZ;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  MarchCtx c;
-  c.ubase = smem;                                // NBUF x UR x RL
-  c.as = smem + NBUF * USZ;                      // UR x TX
-  c.bs = c.as + UR * TX;                         // UR x TX (unused for MASS)
-  c.corr = c.as + UR * TX * (MASS ? 1 : 2);      // NCORR x 2W wall-row corrections
-  c.lane = threadIdx.x & 63;
-  c.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  c.x0 = blockIdx.x * TX;
-  c.y0 = a.out_y0 + blockIdx.y * G::TY;
-  c.zc0 = a.out_z0 + blockIdx.z * a.zchunk;
-  c.zc1 = min(c.zc0 + a.zchunk, a.out_z1);
-  c.x = c.x0 + c.lane;
-  c.ny_out = a.out_y1 - a.out_y0;
-  c.zs = max(c.zc0 - P, a.in_z0);
-  c.ze = min(c.zc1 + P, a.in_z1);  // input planes with contributions: [zs, ze)
-  c.zend = c.zc1 + P;              // retire up to output plane zc1 - 1
-  c.ybase = c.y0 + c.wv * R;       // first output row of this wave
-
-  // x rows: wave-uniform Toeplitz row; the p+1 columns next to each wall
-  // (every column of a domain narrower than 2p + 3) add row(x) - T from a
-  // per-tile LDS table
-  c.need_corr = (c.x0 < a.x_corr_left) || (c.x0 + TX > a.Nx - a.x_corr_right);
-  c.cslot = -1;
-  if (c.need_corr) {
-    if (c.x < a.x_corr_left)
-      c.cslot = c.x;
-    else if (c.x < a.Nx && c.x >= a.Nx - a.x_corr_right)
-      c.cslot = (P + 1) + (c.x - (a.Nx - a.x_corr_right));
-    for (int e = threadIdx.x; e < G::NCORR * 2 * W; e += G::NT) c.corr[e] = a.corrX[e];
+template <int P, int R, int NC, int NP, int BK, int CH>
+__device__ __forceinline__ void producer7(const StencilArgs &a, const Tile7 &t) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  ldouble *u[2] = {t.u0, t.u0 + G::USZ};
+  // prologue: planes zs, zs+1 in flight; x-sweep zs; plane zs+2 into the freed slot
+  if (t.zs < t.ze) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs, u[0]);
+  if (t.zs + 1 < t.ze) {
+    stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + 1, u[1]);
+    wait_dma_plane<0, P, R, NC, NP, BK, CH>(t.wv);
+  } else {
+    GDM_WAIT_VMCNT(0);
   }
+  if (t.zs < t.ze) {
+    xsweep7<P, R, NC, NP, BK>(a, t, u[0], t.ab0);
+    if (t.zs + 2 < t.ze) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + 2, u[0]);
+    }
+  }
+  GDM_LDS_BARRIER();
+  for (int zz = t.zs; zz < t.ze; ++zz) {
+    const int q = zz + 1;  // plane swept in this iteration
+    if (q < t.ze) {
+      if (GDM_DBG(a, 8))
+        ;
+      else if (q + 1 < t.ze)
+        wait_dma_plane<0, P, R, NC, NP, BK, CH>(t.wv);
+      else
+        GDM_WAIT_VMCNT(0);
+      const int s = (q - t.zs) & 1;
+      if (!GDM_DBG(a, 4)) xsweep7<P, R, NC, NP, BK>(a, t, u[s], t.ab0 + s * G::ABSZ);
+      if (q + 2 < t.ze && !GDM_DBG(a, 8)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stage_plane7<P, R, NC, NP, BK, CH>(a, t, q + 2, u[s]);
+      }
+    }
+    if (!GDM_DBG(a, 16)) GDM_LDS_BARRIER();
+  }
+}
 
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void consumer7(const StencilArgs &a, const Tile7 &t) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  constexpr int W = G::W;
+  const int ybase = t.y0 + (t.wv - NP) * R;
+  const bool ytoep = a.y_toep && (ybase >= P + 1) && (ybase + R - 1 + P + 2 <= a.Ny);
+  const bool full = (t.x0 + G::TX <= a.Nx) && (ybase + R <= a.out_y1);
   double acc[W][R];
 #pragma unroll
   for (int s = 0; s < W; ++s)
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
+  GDM_LDS_BARRIER();
+  for (int zb = t.zs; zb < t.zend; zb += W) cblock7<0, P, R, NC, NP, BK>(a, t, ytoep, ybase, full, acc, zb);
+}
 
-  // prologue: NBUF-1 planes in flight
-#pragma unroll
-  for (int d = 0; d < NBUF - 1; ++d)
-    if (c.zs + d < c.ze)
-      stage_plane<P, R, NW, CH>(a, c.zs + d, c.x0, c.y0, c.ubase + ((c.zs + d) % NBUF) * USZ, c.wv, c.lane);
-
-  for (int zb = c.zs - (c.zs % W); zb < c.zend; zb += W)
-    march_phases<0, P, R, NW, NBUF, WPC, MASS, CH>(a, c, acc, zb);
+template <int P, int R, int NC, int NP, int BK, int CH>
+__global__ void __launch_bounds__(64 * (NP + NC), (64 * (NP + NC)) / 256) stencil7_kernel(StencilArgs a) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  ldouble *lds = (ldouble *)smem;
+  Tile7 t;
+  t.u0 = lds;
+  t.ab0 = lds + G::OFF_AB;
+  t.zt = lds + G::OFF_ZT;
+  t.yc = lds + G::OFF_YC;
+  t.corr = lds + G::OFF_CORR;
+  t.lane = threadIdx.x & 63;
+  t.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  t.x0 = blockIdx.x * G::TX;
+  t.y0 = a.out_y0 + blockIdx.y * G::TY;
+  t.zc0 = a.out_z0 + blockIdx.z * a.zchunk;
+  t.zc1 = min(t.zc0 + a.zchunk, a.out_z1);
+  t.zs = max(t.zc0 - P, a.in_z0);
+  t.ze = min(t.zc1 + P, a.in_z1);
+  t.zend = t.zc1 + P;
+  {
+    const int L = a.x_corr_left, rb = a.Nx - a.x_corr_right;
+    t.nl = max(0, min(L, t.x0 + G::TX) - t.x0);
+    t.rs = max(rb, t.x0);
+    const int nr = max(0, min(a.Nx, t.x0 + G::TX) - t.rs);
+    t.ncw = t.nl + nr;
+  }
+  // tables into LDS (ordered before the first use by the prologue barrier)
+  for (int e = threadIdx.x; e < G::ZTSZ; e += G::NT) t.zt[e] = a.zt[e];
+  if (t.ncw > 0)
+    for (int e = threadIdx.x; e < G::CORRSZ; e += G::NT) t.corr[e] = a.corrX[e];
+  // tiles with rows next to a y wall: their column coefficients, pair (t1, t3)
+  // per (tile row r, tap k); global table row = y0 + r (tables are padded by p)
+  if (!(a.y_toep && t.y0 >= P + 1 && t.y0 + G::TY - 1 + P + 2 <= a.Ny))
+    for (int e = threadIdx.x; e < G::UR * G::W; e += G::NT) {
+      const int r = e / G::W, k = e - r * G::W;
+      t.yc[2 * e] = a.yT1[(size_t)(t.y0 + r) * G::W + k];
+      t.yc[2 * e + 1] = a.yT3[(size_t)(t.y0 + r) * G::W + k];
+    }
+  if (t.wv < NP)
+    producer7<P, R, NC, NP, BK, CH>(a, t);
+  else
+    consumer7<P, R, NC, NP, BK>(a, t);
 }
 
 // ---------------------------------------------------------------------------
@@ -410,13 +635,14 @@ __global__ void __launch_bounds__(256) zero_kernel(int64_t n, double *__restrict
 // ---------------------------------------------------------------------------
 // host-side launchers (called from gdm_capi.cpp)
 // ---------------------------------------------------------------------------
-template <int P, int R, int NW, int NBUF, int WPC, bool MASS, int CH>
-static hipError_t launch_stencil_t(const StencilArgs &a, hipStream_t st) {
-  using G = StencilGeom<P, R, NW, NBUF, WPC>;
-  const size_t lds = G::lds_bytes(MASS);
+template <int P, int R, int NC, int NP, int BK, int CH>
+static hipError_t launch7_t(const StencilArgs &a, hipStream_t st) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget");
+  const size_t lds = G::lds_bytes();
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)stencil3d_kernel<P, R, NW, NBUF, WPC, MASS, CH>,
+    hipError_t e = hipFuncSetAttribute((const void *)stencil7_kernel<P, R, NC, NP, BK, CH>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -424,34 +650,36 @@ static hipError_t launch_stencil_t(const StencilArgs &a, hipStream_t st) {
   dim3 grid((a.Nx + G::TX - 1) / G::TX, (a.out_y1 - a.out_y0 + G::TY - 1) / G::TY,
             (a.out_z1 - a.out_z0 + a.zchunk - 1) / a.zchunk);
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return hipSuccess;
-  hipLaunchKernelGGL((stencil3d_kernel<P, R, NW, NBUF, WPC, MASS, CH>), grid, dim3(G::NT), lds, st, a);
+  hipLaunchKernelGGL((stencil7_kernel<P, R, NC, NP, BK, CH>), grid, dim3(G::NT), lds, st, a);
   return hipGetLastError();
 }
 
-template <int P, int R, int NW, int NBUF, int WPC>
-static hipError_t launch_stencil_p(bool mass, const StencilArgs &a, hipStream_t st) {
+template <int P, int R, int NC, int NP>
+static hipError_t launch7_p(int bk, const StencilArgs &a, hipStream_t st) {
   // 16-B LDS-DMA chunks need every staged row to start 16-B aligned
   const bool vec = (a.Nx % 2 == 0) && ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0);
-  if (vec)
-    return mass ? launch_stencil_t<P, R, NW, NBUF, WPC, true, 16>(a, st)
-                : launch_stencil_t<P, R, NW, NBUF, WPC, false, 16>(a, st);
-  return mass ? launch_stencil_t<P, R, NW, NBUF, WPC, true, 4>(a, st)
-              : launch_stencil_t<P, R, NW, NBUF, WPC, false, 4>(a, st);
+  switch (bk) {
+    case 0: return vec ? launch7_t<P, R, NC, NP, 0, 16>(a, st) : launch7_t<P, R, NC, NP, 0, 4>(a, st);
+    case 1: return vec ? launch7_t<P, R, NC, NP, 1, 16>(a, st) : launch7_t<P, R, NC, NP, 1, 4>(a, st);
+    case 2: return vec ? launch7_t<P, R, NC, NP, 2, 16>(a, st) : launch7_t<P, R, NC, NP, 2, 4>(a, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace gdmk
 
+// <P, R, NC, NP>: R output rows per consumer wave, NC consumer and NP producer
+// waves -> tile 64 x (R NC)
+extern "C" int gdmk_stencil_tile_rows(int p) { return p <= 5 ? 32 : 16; }
 
-extern "C" int gdmk_stencil_tile_rows(int p) { return 16; }
-
-extern "C" hipError_t gdmk_launch_stencil(int p, bool mass, const gdmk::StencilArgs &a, hipStream_t st) {
+extern "C" hipError_t gdmk_launch_stencil(int p, int bk, const gdmk::StencilArgs &a, hipStream_t st) {
   using namespace gdmk;
-  switch (p) {  // <P, R, NW, NBUF, WG per CU>
-    case 1: return launch_stencil_p<1, 2, 8, 3, 2>(mass, a, st);
-    case 3: return launch_stencil_p<3, 2, 8, 3, 2>(mass, a, st);
-    case 5: return launch_stencil_p<5, 2, 8, 3, 2>(mass, a, st);
-    case 7: return launch_stencil_p<7, 2, 8, 2, 2>(mass, a, st);
-    case 9: return launch_stencil_p<9, 2, 8, 2, 1>(mass, a, st);
+  switch (p) {
+    case 1: return launch7_p<1, 4, 8, 8>(bk, a, st);
+    case 3: return launch7_p<3, 4, 8, 8>(bk, a, st);
+    case 5: return launch7_p<5, 4, 8, 8>(bk, a, st);
+    case 7: return launch7_p<7, 2, 8, 8>(bk, a, st);
+    case 9: return launch7_p<9, 2, 8, 8>(bk, a, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -10,7 +10,7 @@ import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgdm_hip.so")
+LIB_PATH = os.environ.get("GDM_HIP_LIB") or os.path.join(PKG_ROOT, "lib", "libgdm_hip.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gdm_hip.h")
 
 GDM_OK = 0
