@@ -55,8 +55,10 @@ struct FaceDir {
   int node_begin = 0, node_end = 1;  // output node range (owned)
   int64_t stride = 0;     // global index stride
   int wmax = 1;
+  int qmax = 1;           // largest q-range of FACE_CHUNK consecutive owned nodes
   int *qs = nullptr, *qc = nullptr;
-  double *w = nullptr;
+  double *w = nullptr;    // [n_nodes][wmax]
+  double *wT = nullptr;   // [wmax][n_nodes]
 };
 
 struct Face {
@@ -370,9 +372,11 @@ void build_faces(gdm_op *op) {
         t.node_end = 1;
         t.stride = 0;
         t.wmax = 1;
+        t.qmax = 1;
         t.qs = keep(op, dev_upload(qs));
         t.qc = keep(op, dev_upload(qc));
         t.w = keep(op, dev_upload(w));
+        t.wT = t.w;
         continue;
       }
       const unsigned nce = (unsigned)op->mesh.n_subdivisions[e];
@@ -393,6 +397,18 @@ void build_faces(gdm_op *op) {
       t.node_end = ne;
       t.stride = stride[e];
       t.wmax = ft.wmax;
+      {
+        std::vector<double> wT((size_t)ft.wmax * ft.n_nodes);
+        for (int i = 0; i < ft.n_nodes; ++i)
+          for (int m = 0; m < ft.wmax; ++m) wT[(size_t)m * ft.n_nodes + i] = ft.w[(size_t)i * ft.wmax + m];
+        t.wT = keep(op, dev_upload(wT));
+        // LDS row length of the step-1 kernel: q-range of each chunk of owned nodes
+        t.qmax = 1;
+        for (int ia = nb; ia < ne; ia += gdmk::FACE_CHUNK) {
+          const int ib = std::min(ne, ia + gdmk::FACE_CHUNK) - 1;
+          t.qmax = std::max(t.qmax, std::min(t.Q, ft.qstart[ib] + ft.wmax) - ft.qstart[ia]);
+        }
+      }
       t.qs = keep(op, dev_upload(ft.qstart));
       t.qc = keep(op, dev_upload(ft.qcount));
       t.w = keep(op, dev_upload(ft.w));
@@ -469,9 +485,10 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
       fa.i1_begin = F.t1.node_begin;
       fa.i1_end = F.t1.node_end;
       fa.qs0 = F.t0.qs;
-      fa.qc0 = F.t0.qc;
-      fa.w0 = F.t0.w;
+      fa.w0T = F.t0.wT;
       fa.wmax0 = F.t0.wmax;
+      fa.ldw0 = F.t0.n_nodes;
+      fa.qmax0 = F.t0.qmax;
       fa.qs1 = F.t1.qs;
       fa.qc1 = F.t1.qc;
       fa.w1 = F.t1.w;

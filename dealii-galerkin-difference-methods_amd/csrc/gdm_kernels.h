@@ -47,14 +47,18 @@ struct FaceArgs {
   const double *U;  // [Q1][Q0] stage boundary values of the face
   int Q0, Q1;
   int i0_begin, i0_end, i1_begin, i1_end;  // owned output nodes
-  const int *qs0, *qc0, *qs1, *qc1;
-  const double *w0, *w1;
-  int wmax0, wmax1;
+  const int *qs0, *qs1, *qc1;
+  const double *w0T;  // [wmax0][ldw0]: weights of t0, node-minor (coalesced over nodes)
+  const double *w1;   // [n_nodes1][wmax1]: weights of t1, node-major (wave-uniform rows)
+  int wmax0, wmax1, ldw0;
+  int qmax0;  // largest q-range of FACE_CHUNK consecutive t0 nodes (LDS row length)
   double *T;  // scratch Q1 x (i0_end - i0_begin)
   double *dst;
   int64_t base, stride0, stride1;  // dst offset of node (i0_begin, i1_begin)
   double scale;
 };
+
+constexpr int FACE_CHUNK = 256;  // t0 nodes per workgroup of the face row kernel
 
 }  // namespace gdmk
 

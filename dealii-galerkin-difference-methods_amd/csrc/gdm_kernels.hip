@@ -544,22 +544,46 @@ __global__ void __launch_bounds__(256) chol_lines_kernel(double *__restrict__ v,
 // factorised over the two tangential directions of the face:
 //   step 1: T[q1][i0] = sum_m U[q1][qs0(i0) + m] w0[i0][m]
 //   step 2: dst(i0, i1) += scale * sum_m w1[i1][m] T[qs1(i1) + m][i0]
+// Step 1 stages ROWS rows of U (the q-range of FACE_CHUNK consecutive nodes)
+// in LDS with coalesced loads; each lane then owns one node and reads its
+// weights node-minor (w0T), so every global access is a contiguous wave row.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) face_step1_kernel(const double *__restrict__ U, int Q0, int Q1, int i0_begin,
-                                                          int n0, const int *__restrict__ qs0,
-                                                          const int *__restrict__ qc0,
-                                                          const double *__restrict__ w0, int wmax0,
-                                                          double *__restrict__ T) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int q1 = blockIdx.y;
-  if (t >= n0 || q1 >= Q1) return;
-  const int i0 = i0_begin + t;
-  const double *u = U + (int64_t)q1 * Q0 + qs0[i0];
-  const double *w = w0 + (int64_t)i0 * wmax0;
-  const int n = qc0[i0];
-  double s = 0.0;
-  for (int m = 0; m < n; ++m) s = fma(u[m], w[m], s);
-  T[(int64_t)q1 * n0 + t] = s;
+template <int ROWS>
+__global__ void __launch_bounds__(FACE_CHUNK) face_step1_kernel(const double *__restrict__ U, int Q0, int Q1,
+                                                                 int i0_begin, int n0,
+                                                                 const int *__restrict__ qs0,
+                                                                 const double *__restrict__ w0T, int wmax0,
+                                                                 int ldw0, int qmax, double *__restrict__ T) {
+  extern __shared__ double sh[];  // [ROWS][qmax]
+  const int c0 = blockIdx.x * FACE_CHUNK;
+  const int q1b = blockIdx.y * ROWS;
+  const int nc = min(FACE_CHUNK, n0 - c0);
+  const int ia = i0_begin + c0;
+  const int qa = qs0[ia];
+  const int nq = min(Q0, qs0[ia + nc - 1] + wmax0) - qa;  // <= qmax (host-checked)
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    if (q1b + r < Q1) {
+      const double *src = U + (int64_t)(q1b + r) * Q0 + qa;
+      for (int e = threadIdx.x; e < nq; e += FACE_CHUNK) sh[r * qmax + e] = src[e];
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x >= nc) return;
+  const int i0 = ia + threadIdx.x;
+  const int b = qs0[i0] - qa;
+  const int mend = min(wmax0, nq - b);  // weights past the node's own count are 0
+  double s[ROWS];
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) s[r] = 0.0;
+  for (int m = 0; m < mend; ++m) {
+    const double w = w0T[(int64_t)m * ldw0 + i0];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) s[r] = fma(w, sh[r * qmax + b + m], s[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r)
+    if (q1b + r < Q1) T[(int64_t)(q1b + r) * n0 + c0 + threadIdx.x] = s[r];
 }
 
 __global__ void __launch_bounds__(256) face_step2_kernel(const double *__restrict__ T, int n0, int i1_begin,
@@ -705,9 +729,22 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
   using namespace gdmk;
   const int n0 = f.i0_end - f.i0_begin;
   if (n0 <= 0 || f.Q1 <= 0 || f.i1_end <= f.i1_begin) return hipSuccess;
-  dim3 g1((n0 + 255) / 256, f.Q1), b(256);
-  hipLaunchKernelGGL(face_step1_kernel, g1, b, 0, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0, f.qc0, f.w0, f.wmax0,
-                     f.T);
+  dim3 b(256);
+  // rows per workgroup: as many as fit 48 KiB of LDS (up to 4)
+  const size_t row_bytes = sizeof(double) * (size_t)f.qmax0;
+  const int rows = row_bytes * 4 <= 48 * 1024 ? 4 : (row_bytes * 2 <= 48 * 1024 ? 2 : 1);
+  if (row_bytes > 48 * 1024) return hipErrorInvalidValue;  // <= (FACE_CHUNK + 2p) (p + 1) doubles in practice
+  dim3 g1((n0 + FACE_CHUNK - 1) / FACE_CHUNK, (f.Q1 + rows - 1) / rows);
+  const size_t lds = row_bytes * rows;
+  if (rows == 4)
+    hipLaunchKernelGGL(face_step1_kernel<4>, g1, dim3(FACE_CHUNK), lds, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
+                       f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
+  else if (rows == 2)
+    hipLaunchKernelGGL(face_step1_kernel<2>, g1, dim3(FACE_CHUNK), lds, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
+                       f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
+  else
+    hipLaunchKernelGGL(face_step1_kernel<1>, g1, dim3(FACE_CHUNK), lds, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
+                       f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
   dim3 g2((n0 + 255) / 256, f.i1_end - f.i1_begin);
   hipLaunchKernelGGL(face_step2_kernel, g2, b, 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1,
                      f.dst, f.base, f.stride0, f.stride1, f.scale);

@@ -84,6 +84,30 @@ def test_advection_apply_vs_cell_loop(dim, p, n, a):
     assert rel(host(y), ref) < RTOL_APPLY
 
 
+@pytest.mark.parametrize("dim,p,n", [(2, 5, (600, 9)), (2, 9, (9, 530)), (3, 5, (300, 7, 6)), (3, 3, (5, 270, 4))])
+def test_advection_inflow_faces_multi_chunk(dim, p, n):
+    """Faces whose tangential node range spans several face-kernel chunks
+    (FACE_CHUNK = 256 nodes per workgroup)."""
+    g = _gdm()
+    a = (0.7, 0.4, -0.3)[:dim]
+    op = g.GdmOperator(dim, p, n, 0.0, 1.0, "advection", params=a)
+    m = O.Mesh(dim, p, list(n), 0.0, 1.0)
+    rng = np.random.default_rng(12)
+    u = rng.uniform(-1, 1, m.n_dofs)
+    bc_ref = rng.uniform(-1, 1, m.n_boundary_points())
+    bc_dev = np.zeros_like(bc_ref)
+    bc_dev[op.bc_reference_order()] = bc_ref
+    ref = m.advection_rhs(a, u, bc_ref)
+    y = op.new_vector(local=False)
+    op.apply(dev(u), y, dev(bc_dev))
+    assert rel(host(y), ref) < RTOL_APPLY
+    # the boundary-data part alone (linearity in u+)
+    ref0 = m.advection_rhs(a, u, np.zeros_like(bc_ref))
+    z = op.new_vector(local=False)
+    op.add_boundary_data(dev(bc_dev), z)
+    assert rel(host(z), ref - ref0) < 1e-11
+
+
 @pytest.mark.parametrize("dim,p,n", CASES_SMALL)
 @pytest.mark.parametrize("nitsche", [0.0, 15.0])
 def test_wave_apply_vs_cell_loop(dim, p, n, nitsche):
