@@ -89,6 +89,12 @@ struct gdm_op {
   double *corrX = nullptr, *yT1 = nullptr, *yT3 = nullptr, *zt = nullptr;
   int x_corr_left = 0, x_corr_right = 0, x_toep = 0, y_toep = 0, z_toep = 0;
   double sx = 0, cy[19] = {0};
+  // v8 variants: E pre-scaled by h_z (sx, cy, corrX's B part, yT3), z table e = M_z / h_z
+  double *corrX8 = nullptr, *yT3_8 = nullptr, *zt8 = nullptr;
+  double *yT1d = nullptr, *yT3d = nullptr, *m_yT3d = nullptr;  // v8 y corrections
+  double sx8 = 0, cy8[19] = {0};
+  double dint = 0, m_dint = 0;  // interior z scales of D (operator, mass)
+  int stencil_version = 8;
   // the same for the mass operator of an advection/wave op (gdm_mass_apply)
   double *m_corrX = nullptr, *m_zt = nullptr;
   double *lrow[3] = {nullptr, nullptr, nullptr}, *invd[3] = {nullptr, nullptr, nullptr};
@@ -240,7 +246,7 @@ void build_tables(gdm_op *op) {
   op->z_toep = toep(2);
   const std::vector<double> mhat = interior_band(p, 0), bhat = interior_band(p, op->kind == GDM_OP_WAVE ? 2 : 1);
   // x wall-column corrections (rows x <= p and x >= n - p use one-sided categories)
-  auto corr_table = [&](const gdm::Band &Mx, const gdm::Band &Bx, int &left, int &right) {
+  auto corr_table = [&](const gdm::Band &Mx, const gdm::Band &Bx, int &left, int &right, double bscale = 1.0) {
     const int n = Mx.n;
     left = std::min(p + 1, n);
     const int right_begin = std::max(p + 1, n - p - 1);
@@ -250,7 +256,7 @@ void build_tables(gdm_op *op) {
       for (int k = 0; k < W; ++k) {
         const double tm = op->x_toep ? h[0] * mhat[k] : 0.0, tb = op->x_toep ? beta[0] * bhat[k] : 0.0;
         corr[(size_t)slot * 2 * W + k] = (Mx(x, x - p + k) - tm) / h[0];
-        corr[(size_t)slot * 2 * W + W + k] = h[1] * (Bx(x, x - p + k) - tb);
+        corr[(size_t)slot * 2 * W + W + k] = bscale * h[1] * (Bx(x, x - p + k) - tb);
       }
     };
     for (int x = 0; x < left; ++x) fill(x, x);
@@ -293,6 +299,34 @@ void build_tables(gdm_op *op) {
   op->zt = mass ? op->m_zt : keep(op, dev_upload(z_table(&M[2], Bz, h[2], beta[2] * h[0] * h[1], bhat)));
   op->sx = h[1] * beta[0];
   for (int k = 0; k < W; ++k) op->cy[k] = h[0] * beta[1] * bhat[k];
+  op->m_dint = h[0] * h[1] * h[2];
+  // v8 y tables: (wall row - Toeplitz row) corrections, column form; zero away
+  // from the walls (the kernel adds them only for waves with wall rows)
+  {
+    auto delta = [&](const gdm::Band &A, const std::vector<double> &toep) {
+      gdm::Band d = A;
+      for (int i = 0; i < A.n; ++i)
+        for (int j = std::max(0, i - p); j <= std::min(A.n - 1, i + p); ++j) d(i, j) = A(i, j) - toep[j - i + p];
+      return d;
+    };
+    std::vector<double> tm(W), tc(W, 0.0);
+    for (int k = 0; k < W; ++k) tm[k] = mhat[k];
+    if (!mass)
+      for (int k = 0; k < W; ++k) tc[k] = h[0] * beta[1] * bhat[k] * h[2];
+    op->yT1d = keep(op, dev_upload(band_cols(delta(scaled(M[1], 1.0 / h[1]), tm), p, ypad)));
+    op->yT3d = keep(op, dev_upload(band_cols(delta(scaled(B[1], h[0] * h[2]), tc), p, ypad)));
+    op->m_yT3d = keep(op, dev_upload(band_cols(gdm::Band(M[1].n, p), p, ypad)));
+  }
+  if (!mass) {
+    int l8 = 0, r8 = 0;
+    op->corrX8 = keep(op, dev_upload(corr_table(M[0], B[0], l8, r8, h[2])));
+    op->yT3_8 = keep(op, dev_upload(band_cols(scaled(B[1], h[0] * h[2]), p, ypad)));
+    const gdm::Band Mz8 = scaled(M[2], 1.0 / h[2]);
+    op->zt8 = keep(op, dev_upload(z_table(&Mz8, Bz, 1.0, beta[2] * h[0] * h[1], bhat)));
+    op->sx8 = op->sx * h[2];
+    op->dint = beta[2] * h[0] * h[1];
+    for (int k = 0; k < W; ++k) op->cy8[k] = op->cy[k] * h[2];
+  }
   // mass operator tables for gdm_mass_apply on a non-mass op
   {
     gdm::Band zero0(M[0].n, p);
@@ -453,10 +487,24 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst)
   const bool as_mass = mass || op->kind == GDM_OP_MASS;
   a.yT1 = op->yT1;
   a.yT3 = op->yT3;
+  // v8 needs every x and y tile to touch at most one wall; smaller meshes use v7
+  int ty8 = 32, wgs8 = 1;
+  gdmk_stencil8_geom(op->p, &ty8, &wgs8);
+  const bool v8 = op->stencil_version == 8 && op->K[1] >= ty8 + 2 * op->p + 2 && op->K[0] >= 64 + 2 * op->p + 2;
+  if (v8) a.yT1 = op->yT1d;
   if (as_mass) {
     a.sx = 0.0;
     a.corrX = op->m_corrX;
     a.zt = op->m_zt;
+    a.dint = op->m_dint;
+    if (v8) a.yT3 = op->m_yT3d;
+  } else if (v8) {
+    a.dint = op->dint;
+    a.sx = op->sx8;
+    for (int k = 0; k < 19; ++k) a.cy[k] = op->cy8[k];
+    a.corrX = op->corrX8;
+    a.yT3 = op->yT3d;
+    a.zt = op->zt8;
   } else {
     a.sx = op->sx;
     for (int k = 0; k < 19; ++k) a.cy[k] = op->cy[k];
@@ -468,7 +516,40 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst)
 #endif
   if (L.n_owned == 0) return hipSuccess;
   const int bk = as_mass ? 0 : (op->kind == GDM_OP_WAVE ? 2 : 1);
-  return gdmk_launch_stencil(op->p, bk, a, op->stream);
+  if (!v8) return gdmk_launch_stencil(op->p, bk, a, op->stream);
+  // v8: output planes whose z columns are all interior (z' in [3p+1, Nz-3p-2])
+  // go to the compile-time-band kernel; the rest (next to the z walls) to the
+  // table kernel, both ranges of it in one launch.
+  const int p = op->p, zlo = 3 * p + 1, zhi = a.Nz - 3 * p - 1;
+  const int i0 = std::max(a.out_z0, zlo), i1 = std::min(a.out_z1, zhi);
+  const bool split = a.z_toep && i1 - i0 >= 2 * p + 1 && !std::getenv("GDM_NO_ZINT");
+  const int ty = ty8, wgs = wgs8;
+  const int64_t tiles = (int64_t)((a.Nx + 63) / 64) * ((a.out_y1 - a.out_y0 + ty - 1) / ty);
+  const char *rounds_env = std::getenv("GDM_ROUNDS");
+  const int rounds = rounds_env ? std::max(1, std::atoi(rounds_env)) : 1;
+  auto zchunk_for = [&](int len) {  // about `rounds` rounds of workgroups on 256 CUs
+    const int64_t chunks = std::max<int64_t>(1, (256 * wgs * rounds + tiles - 1) / tiles);
+    return (int)std::max<int64_t>(std::min(len, 8), (len + chunks - 1) / chunks);
+  };
+  if (!split) {
+    a.cz0[0] = a.out_z0; a.cz1[0] = a.out_z1; a.cz0[1] = a.cz1[1] = 0;
+    a.zchunk = zchunk_for(a.out_z1 - a.out_z0);
+    a.nchunk0 = (a.cz1[0] - a.cz0[0] + a.zchunk - 1) / a.zchunk;
+    return gdmk_launch_stencil8(p, bk, false, a, op->stream);
+  }
+  gdmk::StencilArgs b = a;
+  b.cz0[0] = i0; b.cz1[0] = i1; b.cz0[1] = b.cz1[1] = 0;
+  b.zchunk = zchunk_for(i1 - i0);
+  b.nchunk0 = (i1 - i0 + b.zchunk - 1) / b.zchunk;
+  hipError_t e = gdmk_launch_stencil8(p, bk, true, b, op->stream);
+  if (e != hipSuccess) return e;
+  // wall ranges [out_z0, i0) and [i1, out_z1)
+  a.cz0[0] = a.out_z0; a.cz1[0] = i0;
+  a.cz0[1] = i1; a.cz1[1] = a.out_z1;
+  a.zchunk = std::max(1, std::max(i0 - a.out_z0, a.out_z1 - i1));
+  a.nchunk0 = i0 > a.out_z0 ? 1 : 0;
+  if (i0 <= a.out_z0 && i1 >= a.out_z1) return hipSuccess;
+  return gdmk_launch_stencil8(p, bk, false, a, op->stream);
 }
 
 void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned) {
@@ -591,6 +672,7 @@ int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int
   build_tables(op);
   build_faces(op);
   op->zchunk = choose_zchunk(op);
+  if (const char *env = std::getenv("GDM_STENCIL")) op->stencil_version = std::atoi(env) == 7 ? 7 : 8;
   hip_check(hipMalloc(&op->dot_partial, sizeof(double) * op->n_dot_partial), "hipMalloc");
   keep(op, op->dot_partial);
   hip_check(hipMalloc(&op->dot_out, sizeof(double)), "hipMalloc");

@@ -38,6 +38,14 @@ struct StencilArgs {
   // z columns [2(2p+1)+1][2p+1][2] = (e, d) pairs, out(zz - p + k) += e E + d D':
   // rows 0..2p: planes 0..2p; rows 2p+1..4p+1: planes Nz-2p-1..Nz-1; row 4p+2: interior
   const double *__restrict__ zt;
+  // v8 only: E arrives pre-scaled by the interior z mass scale (sx, cy, corrX's
+  // B part and yT3 carry it), interior z planes use the compile-time bands
+  // out(zz - p + k) += mhat[k] E + dint dhat[2p - k] D, and zt's wall rows hold
+  // (M_z / h_z, B_z) pairs.
+  double dint;
+  // v8 only: output plane ranges computed by this launch (chunks of zchunk
+  // planes; blockIdx.z < nchunk0 -> range 0, else range 1)
+  int cz0[2], cz1[2], nchunk0;
   int dbg;  // diagnostic builds only (-DGDM_DIAG): bits disable kernel phases
 };
 
@@ -64,7 +72,10 @@ constexpr int FACE_CHUNK = 256;  // t0 nodes per workgroup of the face row kerne
 
 extern "C" {
 hipError_t gdmk_launch_stencil(int p, int bk, const gdmk::StencilArgs &a, hipStream_t st);
+// zint: every z column of the launch's planes is interior (compile-time z bands)
+hipError_t gdmk_launch_stencil8(int p, int bk, bool zint, const gdmk::StencilArgs &a, hipStream_t st);
 int gdmk_stencil_tile_rows(int p);
+void gdmk_stencil8_geom(int p, int *tile_rows, int *wgs_per_cu);
 hipError_t gdmk_launch_chol_lines(int p, double *v, int len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,
                                   int64_t C, const double *lrow, const double *inv_diag, hipStream_t st);
 hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st);

@@ -24,6 +24,14 @@
 #include "gdm_coeffs.h"
 #include "gdm_kernels.h"
 
+#ifndef GDM_R5
+#define GDM_R5 4
+#define GDM_NC5 8
+#define GDM_NP5 8
+#endif
+#ifndef GDM_PF5
+#define GDM_PF5 2
+#endif
 namespace gdmk {
 
 
@@ -122,7 +130,8 @@ typedef __attribute__((address_space(3))) const dpair lcdouble2;
   } while (0)
 
 struct Tile7 {
-  ldouble *u0, *ab0, *zt, *yc, *corr;
+  ldouble *u0, *ab0, *zt, *yc, *corr, *yw;
+  bool yedge;  // v8: the tile has rows next to a y wall
   int lane, wv, x0, y0, zc0, zc1, zs, ze, zend;
   // x wall columns inside this tile: nl from the left wall, nr from column rs on
   int nl, rs, ncw;
@@ -494,6 +503,558 @@ __global__ void __launch_bounds__(64 * (NP + NC), (64 * (NP + NC)) / 256) stenci
     consumer7<P, R, NC, NP, BK>(a, t);
 }
 
+// ===========================================================================
+// Fused Kronecker stencil, v8.  Same roles and tiles as v7, re-balanced for
+// latency:
+//   * each producer wave keeps a 3-slot LDS-DMA ring of its own row groups,
+//     so two planes are in flight at every wait (v7: one),
+//   * the x-sweep results stay in registers until the single interleaved
+//     (A, B) plane buffer is free; two barriers per plane:
+//       producer  X(i) | F_i | write AB(i) | L_i | DMA(i + 3)
+//       consumer  L_i | Y(i) | F_i+1 | Z(i)
+//     (X(i+1) overlaps Y(i), the AB write overlaps Z(i)),
+//   * consumers read (A, B) pairs with one ds_read_b128, PF rows ahead,
+//   * interior z planes use the compile-time bands (E arrives pre-scaled by
+//     the z mass scale, D is scaled by dint): no LDS reads in the z phase;
+//     only the 2(2p+1) wall planes read the LDS column table.
+// ===========================================================================
+template <int P, int R, int NC, int NP, int BK>
+struct Geom8 {
+  static constexpr int W = 2 * P + 1;
+  static constexpr int TX = 64;
+  static constexpr int TY = R * NC;
+  static constexpr int UR = TY + 2 * P;
+  static constexpr int XH = P + 1;
+  static constexpr int RL0 = TX + 2 * XH;
+  static constexpr int RL = (RL0 % 4 == 2) ? RL0 : RL0 + 2;
+  static constexpr int NW = NP + NC;
+  static constexpr int NT = 64 * NW;
+  static constexpr int NG = (UR + 3) / 4;
+  static constexpr int NPASS = (NG + NP - 1) / NP;
+  static constexpr int USZ = NG * 4 * RL;
+  static constexpr int NAB = BK == 0 ? 1 : 2;
+  static constexpr int ABSZ = UR * TX * NAB;
+  static constexpr int ZTSZ = (2 * W + 1) * W * 2;  // wall planes + interior row
+  static constexpr int YCSZ = UR * W * 2;
+  static constexpr int CORRSZ = 2 * (P + 1) * 2 * W;
+  static constexpr int NWIN = 2 * P + 6;
+  // workgroups per CU the tile is sized for (<= 12 waves: two) and the DMA
+  // ring depth that fits that LDS share (3 slots if possible, else 2)
+  static constexpr int WGS = NW <= 12 ? 2 : 1;
+  static constexpr size_t LDS_CAP = (160 * 1024) / WGS;
+  static constexpr int NSLOT =
+      sizeof(double) * (size_t)(3 * USZ + ABSZ + ZTSZ + YCSZ + CORRSZ + (P + 1) * TX * NAB) <= LDS_CAP ? 3 : 2;
+  static constexpr int YWSZ = (P + 1) * TX * NAB;  // y-wall corrections of one plane
+  static constexpr int OFF_AB = NSLOT * USZ;
+  static constexpr int OFF_ZT = OFF_AB + ABSZ;
+  static constexpr int OFF_YC = OFF_ZT + ZTSZ;
+  static constexpr int OFF_CORR = OFF_YC + YCSZ;
+  static constexpr int OFF_YW = OFF_CORR + CORRSZ;
+  static constexpr size_t lds_bytes() { return sizeof(double) * (size_t)(OFF_YW + YWSZ); }
+};
+
+// the z-direction interior band of operator kind BK (column form index 2p - k)
+template <int P, int BK>
+__device__ __forceinline__ constexpr double zband(int k) {
+  using IR = InteriorRows<P>;
+  return BK == 0 ? IR::m[2 * P - k] : (BK == 1 ? IR::c[2 * P - k] : IR::l[2 * P - k]);
+}
+
+// wait until at most K planes of DMA of this producer wave are in flight
+template <int I, int K, int P, int R, int NC, int NP, int BK, int CH>
+__device__ __forceinline__ void wait_dma_planes(int wv) {
+  if constexpr (I < NP) {
+    if (wv == I) {
+      GDM_WAIT_VMCNT((K * Dma7<P, R, NC, NP, BK, CH>::nd(I)));
+      return;
+    }
+    wait_dma_planes<I + 1, K, P, R, NC, NP, BK, CH>(wv);
+  }
+}
+
+// x-sweep of row group g (pass of this producer wave) into registers:
+// A = mhat*u (+ wall rows), B = sx bhat*u (+ wall rows), 4 consecutive x per lane
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void xsweep8(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g, double (&A)[4],
+                                        double (&B)[4]) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  using IR = InteriorRows<P>;
+  constexpr int W = G::W, RL = G::RL;
+  const int rr = t.lane >> 4, q = t.lane & 15;
+  const int r = 4 * g + rr;
+  lcdouble2 *wp = (lcdouble2 *)(us + r * RL + 4 * q);
+  double w[G::NWIN];
+#pragma unroll
+  for (int i = 0; i < G::NWIN / 2; ++i) {
+    const dpair v = wp[i];
+    w[2 * i] = v.x;
+    w[2 * i + 1] = v.y;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) A[j] = B[j] = 0.0;
+  if (a.x_toep) {
+#pragma unroll
+    for (int k = 0; k < W; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        A[j] = fma(IR::m[k], w[j + k + 1], A[j]);
+        if constexpr (BK == 1) B[j] = fma(IR::c[k], w[j + k + 1], B[j]);
+        if constexpr (BK == 2) B[j] = fma(IR::l[k], w[j + k + 1], B[j]);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) B[j] *= a.sx;
+}
+
+// Wall columns of row group g (first / last x tiles only): the
+// (wall row - Toeplitz row) corrections of M_x and B_x, one (row, column,
+// component) item per lane so the work is spread over the wave instead of
+// serialised per lane.  xwall8_calc runs before F (overlapping the consumers'
+// y-sweep); xwall8_add adds the values into AB after write_ab8 of the group
+// (same wave: LDS operations stay in program order).
+template <int P, int BK>
+struct XWall {
+  static constexpr int NCOMP = BK == 0 ? 1 : 2;
+  static constexpr int NI = (4 * (P + 1) * NCOMP + 63) / 64;  // items per lane (one x wall per tile)
+  double v[NI];
+  int o[NI];  // AB offset, -1: none
+};
+
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void xwall8_calc(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g,
+                                            XWall<P, BK> &xw) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  constexpr int W = G::W, RL = G::RL, TX = G::TX, NCOMP = XWall<P, BK>::NCOMP;
+  const int nitems = 4 * t.ncw * NCOMP;
+#pragma unroll
+  for (int it = 0; it < XWall<P, BK>::NI; ++it) {
+    const int e = t.lane + 64 * it;
+    xw.o[it] = -1;
+    xw.v[it] = 0.0;
+    const int comp = e % NCOMP, rest = e / NCOMP;
+    const int idx = rest % max(t.ncw, 1), rr = rest / max(t.ncw, 1);
+    const int r = 4 * g + rr;
+    if (e < nitems && r < G::UR) {
+      const int x = idx < t.nl ? t.x0 + idx : t.rs + (idx - t.nl);
+      const int cs = x < a.x_corr_left ? x : (P + 1) + (x - (a.Nx - a.x_corr_right));
+      const int lx = x - t.x0;
+      lcdouble *ur = us + r * RL + lx + 1;  // tap k of column x
+      lcdouble *cm = t.corr + cs * 2 * W + comp * W;
+      double d = 0.0;
+#pragma unroll
+      for (int k = 0; k < W; ++k) d = fma(cm[k], ur[k], d);
+      xw.v[it] = d;
+      xw.o[it] = BK != 0 ? (r * TX + lx) * 2 + comp : r * TX + lx;
+    }
+  }
+}
+
+template <int P, int BK>
+__device__ __forceinline__ void xwall8_add(const Tile7 &t, const XWall<P, BK> &xw) {
+#pragma unroll
+  for (int it = 0; it < XWall<P, BK>::NI; ++it)
+    if (xw.o[it] >= 0) t.ab0[xw.o[it]] += xw.v[it];
+}
+
+// store row group g's (A, B) into the interleaved plane buffer
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void write_ab8(const Tile7 &t, int g, const double (&A)[4], const double (&B)[4]) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  constexpr int TX = G::TX;
+  const int rr = t.lane >> 4, q = t.lane & 15;
+  const int r = 4 * g + rr;
+  if (r < G::UR) {
+    if constexpr (BK != 0) {
+      ldouble2 *p = (ldouble2 *)(t.ab0 + (r * TX + 4 * q) * 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[j] = dpair{A[j], B[j]};
+    } else {
+      ldouble2 *p = (ldouble2 *)(t.ab0 + r * TX + 4 * q);
+      p[0] = dpair{A[0], A[1]};
+      p[1] = dpair{A[2], A[3]};
+    }
+  }
+}
+
+// first / end wall row of this tile's y-wall block (tile rows [y0, y0 + TY));
+// begin = -1: no wall row in the tile
+template <int P, int TY>
+__device__ __forceinline__ int ywall_begin(const StencilArgs &a, int y0) {
+  if (y0 <= P) return y0;                                          // bottom wall rows [0, p]
+  if (y0 + TY - 1 >= a.Ny - P - 1) return max(y0, a.Ny - P - 1);  // top wall rows
+  return -1;
+}
+template <int P, int TY>
+__device__ __forceinline__ int ywall_end(const StencilArgs &a, int y0) {
+  if (y0 <= P) return min(y0 + TY, P + 1);
+  return min(y0 + TY, a.Ny);
+}
+
+// y-wall corrections of plane AB (edge tiles only, between L_i and M_i): for
+// the wall rows y of this tile dD(y) = sum_s c1(y, s) A(s) and
+// dE(y) = sum_s c1 B(s) + c3 A(s) with the (wall - Toeplitz) column tables;
+// one row per producer wave, lane = x
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void ywall8(const StencilArgs &a, const Tile7 &t) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  constexpr int W = G::W, TX = G::TX;
+  const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
+  // rows go to the producer waves from the last one down: the first waves
+  // may own a second row group
+  for (int y = yb + (NP - 1 - t.wv); y < ye; y += NP) {
+    const int wi = y - yb;
+    double dD = 0.0, dE = 0.0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const int rs = y + 2 * P - k - t.y0;  // tile row of input s = y + p - k
+      const dpair c = ((lcdouble2 *)t.yc)[rs * W + k];
+      if constexpr (BK != 0) {
+        const dpair v = ((lcdouble2 *)t.ab0)[rs * TX + t.lane];
+        dD = fma(c.x, v.x, dD);
+        dE = fma(c.x, v.y, fma(c.y, v.x, dE));
+      } else {
+        dD = fma(c.x, t.ab0[rs * TX + t.lane], dD);
+      }
+    }
+    if constexpr (BK != 0)
+      ((ldouble2 *)t.yw)[wi * TX + t.lane] = dpair{dD, dE};
+    else
+      t.yw[wi * TX + t.lane] = dD;
+  }
+}
+
+template <int P, int R, int NC, int NP, int BK, int CH>
+__device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  constexpr int NS = G::NSLOT;
+  ldouble *u[3] = {t.u0, t.u0 + G::USZ, t.u0 + (NS > 2 ? 2 : 0) * G::USZ};
+  const int n = t.ze - t.zs;
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+    if (k < n) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + k, u[k]);
+  GDM_LDS_BARRIER();  // tables in LDS
+  double AR[4], BR[4];
+  int slot = 0;
+  for (int i = 0; i < n; ++i) {
+    const int rem = n - 1 - i;  // planes issued after plane i (at most NS - 1)
+    if (GDM_DBG(a, 8))
+      ;
+    else if (NS > 2 && rem >= 2)
+      wait_dma_planes<0, 2, P, R, NC, NP, BK, CH>(t.wv);
+    else if (rem == 1)
+      wait_dma_planes<0, 1, P, R, NC, NP, BK, CH>(t.wv);
+    else
+      GDM_WAIT_VMCNT(0);
+    // the first two row groups into registers before F (overlapping the
+    // consumers' y-sweep of plane i - 1), any further ones straight into AB
+    double AR2[4], BR2[4];
+    if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], t.wv, AR, BR);
+    const bool two = G::NPASS > 1 && t.wv + NP < G::NG;
+    if (two && !GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], t.wv + NP, AR2, BR2);
+    XWall<P, BK> xw0, xw1;
+    if (t.ncw > 0) {
+      xwall8_calc<P, R, NC, NP, BK>(a, t, u[slot], t.wv, xw0);
+      if (two) xwall8_calc<P, R, NC, NP, BK>(a, t, u[slot], t.wv + NP, xw1);
+    }
+    if (t.yedge && i > 0) {
+      ywall8<P, R, NC, NP, BK>(a, t);  // corrections of plane i - 1 (AB still holds it)
+      GDM_LDS_BARRIER();               // M_i-1
+    }
+    GDM_LDS_BARRIER();  // F_i
+    write_ab8<P, R, NC, NP, BK>(t, t.wv, AR, BR);
+    if (two) write_ab8<P, R, NC, NP, BK>(t, t.wv + NP, AR2, BR2);
+    if (t.ncw > 0) {
+      xwall8_add<P, BK>(t, xw0);
+      if (two) xwall8_add<P, BK>(t, xw1);
+    }
+#pragma unroll
+    for (int ps = 2; ps < G::NPASS; ++ps) {
+      const int g = t.wv + ps * NP;
+      if (g < G::NG) {
+        if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], g, AR, BR);
+        write_ab8<P, R, NC, NP, BK>(t, g, AR, BR);
+        if (t.ncw > 0) {
+          xwall8_calc<P, R, NC, NP, BK>(a, t, u[slot], g, xw0);
+          xwall8_add<P, BK>(t, xw0);
+        }
+      }
+    }
+    GDM_LDS_BARRIER();  // L_i: AB(i) loaded
+    if (i + NS < n && !GDM_DBG(a, 8)) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + NS, u[slot]);
+    slot = slot == NS - 1 ? 0 : slot + 1;
+  }
+  if (t.yedge && n > 0) {
+    ywall8<P, R, NC, NP, BK>(a, t);
+    GDM_LDS_BARRIER();  // M_n-1
+  }
+  GDM_LDS_BARRIER();  // F_n
+}
+
+// y-sweep of the consumer's R rows from the (A, B) plane: D' and E with the
+// compile-time interior bands, rows read PF ahead of their use (wall rows get
+// their corrections from the producers' ywall8, see cplane8).
+template <int P, int R, int NC, int NP, int BK, int PF>
+__device__ __forceinline__ void ysweep8(const StencilArgs &a, const Tile7 &t, double (&D)[R], double (&E)[R]) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  using IR = InteriorRows<P>;
+  constexpr int W = G::W, TX = G::TX, NR = R + 2 * P;
+  const int row0 = (t.wv - NP) * R;
+#pragma unroll
+  for (int j = 0; j < R; ++j) D[j] = E[j] = 0.0;
+  if constexpr (BK != 0) {
+    lcdouble2 *vp = (lcdouble2 *)t.ab0 + row0 * TX + t.lane;
+    dpair v[NR];
+#pragma unroll
+    for (int s = 0; s < PF && s < NR; ++s) v[s] = vp[s * TX];
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      GDM_FENCE();
+      if (s + PF < NR) v[s + PF] = vp[(s + PF) * TX];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int k = s - j;  // row form: M(y_j, y_j - p + k)
+        if (k >= 0 && k < W) {
+          D[j] = fma(IR::m[k], v[s].x, D[j]);
+          E[j] = fma(IR::m[k], v[s].y, fma(a.cy[k], v[s].x, E[j]));
+        }
+      }
+    }
+  } else {
+    const volatile lcdouble *vp = t.ab0 + row0 * TX + t.lane;
+    double v[NR];
+#pragma unroll
+    for (int s = 0; s < PF && s < NR; ++s) v[s] = vp[s * TX];
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      GDM_FENCE();
+      if (s + PF < NR) v[s + PF] = vp[(s + PF) * TX];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int k = s - j;
+        if (k >= 0 && k < W) D[j] = fma(IR::m[k], v[s], D[j]);
+      }
+    }
+  }
+}
+
+template <int JP, int P, int R, int NC, int NP, int BK, int PF, bool WALL, bool YW>
+__device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, int ybase, bool full,
+                                        double (&acc)[2 * P + 1][R], int zz) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  using IR = InteriorRows<P>;
+  constexpr int W = G::W;
+  if (zz < t.ze) {
+    double D[R], E[R];
+    GDM_LDS_BARRIER();  // L_i
+    if (GDM_DBG(a, 1)) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) D[j] = E[j] = (double)zz;
+    } else {
+      ysweep8<P, R, NC, NP, BK, PF>(a, t, D, E);
+    }
+    if constexpr (YW) {
+      GDM_LDS_BARRIER();  // M_i
+      const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int y = ybase + j;
+        if (y >= yb && y < ye) {
+          if constexpr (BK != 0) {
+            const dpair c = ((lcdouble2 *)t.yw)[(y - yb) * G::TX + t.lane];
+            D[j] += c.x;
+            E[j] += c.y;
+          } else {
+            D[j] += t.yw[(y - yb) * G::TX + t.lane];
+          }
+        }
+      }
+    }
+    GDM_LDS_BARRIER();  // F_i+1
+    if (!GDM_DBG(a, 2)) {
+      if constexpr (!WALL) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) D[j] *= a.dint;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          GDM_FENCE();
+          const int slot = (JP - P + k + 2 * W) % W;
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            if constexpr (BK == 0)
+              acc[slot][j] = fma(zband<P, BK>(k), D[j], acc[slot][j]);
+            else
+              acc[slot][j] = fma(IR::m[k], E[j], fma(zband<P, BK>(k), D[j], acc[slot][j]));
+          }
+        }
+      } else {
+        // wall blocks: every plane from the column table (row 2W = interior)
+        const int row = zz < W ? zz : (zz >= a.Nz - W ? W + zz - (a.Nz - W) : 2 * W);
+#ifdef GDM_EXP_SZT
+        cdouble *zg = cptr(a.zt) + row * W * 2;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          const double ce = zg[2 * k], cd = zg[2 * k + 1];
+          const int slot = (JP - P + k + 2 * W) % W;
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            if constexpr (BK == 0)
+              acc[slot][j] = fma(cd, D[j], acc[slot][j]);
+            else
+              acc[slot][j] = fma(ce, E[j], fma(cd, D[j], acc[slot][j]));
+          }
+        }
+        if (false) {
+#else
+        {
+#endif
+        lcdouble2 *zc = (lcdouble2 *)t.zt + row * W;
+        dpair cur = zc[0];
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          GDM_FENCE();
+          const dpair nxt = zc[k + 1 < W ? k + 1 : k];
+          const int slot = (JP - P + k + 2 * W) % W;
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            if constexpr (BK == 0)
+              acc[slot][j] = fma(cur.y, D[j], acc[slot][j]);
+            else
+              acc[slot][j] = fma(cur.x, E[j], fma(cur.y, D[j], acc[slot][j]));
+          }
+          cur = nxt;
+        }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < W; ++s)
+#pragma unroll
+    for (int j = 0; j < R; ++j) asm volatile("" : "+v"(acc[s][j]));
+  // retire output plane zz - p
+  constexpr int rslot = (JP - P + 2 * W) % W;
+  const int zo = zz - P;
+  if (zo >= t.zc0 && zo < t.zc1) {
+    const int Nx = a.Nx, x = t.x0 + t.lane;
+    double *orow = a.dst + ((int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) + (ybase - a.out_y0)) * Nx + x;
+    if (full) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) orow[(int64_t)j * Nx] = acc[rslot][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (x < Nx && ybase + j < a.out_y1) orow[(int64_t)j * Nx] = acc[rslot][j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
+}
+
+template <int JP, int P, int R, int NC, int NP, int BK, int PF, bool WALL, bool YW>
+__device__ __forceinline__ void cblock8(const StencilArgs &a, const Tile7 &t, int ybase, bool full,
+                                        double (&acc)[2 * P + 1][R], int zb) {
+  if constexpr (JP < 2 * P + 1) {
+    cplane8<JP, P, R, NC, NP, BK, PF, WALL, YW>(a, t, ybase, full, acc, zb + JP);
+    cblock8<JP + 1, P, R, NC, NP, BK, PF, WALL, YW>(a, t, ybase, full, acc, zb);
+  }
+}
+
+template <int P, int R, int NC, int NP, int BK, int PF, bool ZI, bool YW>
+__device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7 &t, int ybase, bool full) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  constexpr int W = G::W;
+  double acc[W][R];
+#pragma unroll
+  for (int s = 0; s < W; ++s)
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
+  GDM_LDS_BARRIER();  // tables in LDS
+  GDM_LDS_BARRIER();  // F_0
+  // ZI: the host launched this kernel only on output planes whose z columns
+  // are all interior -> compile-time z bands, no table reads; otherwise every
+  // plane reads its column (wall columns or the interior one) from LDS
+  for (int zb = t.zs; zb < t.zend; zb += W)
+    cblock8<0, P, R, NC, NP, BK, PF, !ZI, YW>(a, t, ybase, full, acc, zb);
+}
+
+template <int P, int R, int NC, int NP, int BK, int PF, bool ZI>
+__device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  const int ybase = t.y0 + (t.wv - NP) * R;
+  const bool full = (t.x0 + G::TX <= a.Nx) && (ybase + R <= a.out_y1);
+  // edge tiles (rows next to a y wall) wait for the producers' y-wall
+  // corrections every plane: their own copy of the loop keeps that out of the
+  // hot block of the other tiles
+  if (t.yedge)
+    consumer8_loop<P, R, NC, NP, BK, PF, ZI, true>(a, t, ybase, full);
+  else
+    consumer8_loop<P, R, NC, NP, BK, PF, ZI, false>(a, t, ybase, full);
+}
+
+template <int P, int R, int NC, int NP, int BK, int CH, int PF, bool ZI>
+__global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, NP, BK>::WGS) / 4)
+    stencil8_kernel(StencilArgs a) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  ldouble *lds = (ldouble *)smem;
+  Tile7 t;
+  t.u0 = lds;
+  t.ab0 = lds + G::OFF_AB;
+  t.zt = lds + G::OFF_ZT;
+  t.yc = lds + G::OFF_YC;
+  t.corr = lds + G::OFF_CORR;
+  t.yw = lds + G::OFF_YW;
+  t.lane = threadIdx.x & 63;
+  t.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  t.x0 = blockIdx.x * G::TX;
+  t.y0 = a.out_y0 + blockIdx.y * G::TY;
+#ifdef GDM_EXP_NOY
+  t.yedge = false;  // timing experiment: wrong next to the y walls
+#else
+  t.yedge = ywall_begin<P, G::TY>(a, t.y0) >= 0;
+#endif
+  {
+    const int r = (int)blockIdx.z < a.nchunk0 ? 0 : 1;
+    const int c = (int)blockIdx.z - (r ? a.nchunk0 : 0);
+    t.zc0 = a.cz0[r] + c * a.zchunk;
+    t.zc1 = min(t.zc0 + a.zchunk, a.cz1[r]);
+  }
+  t.zs = max(t.zc0 - P, a.in_z0);
+  t.ze = min(t.zc1 + P, a.in_z1);
+  t.zend = t.zc1 + P;
+  {
+    const int L = a.x_corr_left, rb = a.Nx - a.x_corr_right;
+    t.nl = max(0, min(L, t.x0 + G::TX) - t.x0);
+    t.rs = max(rb, t.x0);
+    const int nr = max(0, min(a.Nx, t.x0 + G::TX) - t.rs);
+    t.ncw = t.nl + nr;
+#ifdef GDM_EXP_NOX
+    t.ncw = 0;  // timing experiment: wrong next to the x walls
+#endif
+  }
+  if (!ZI)
+    for (int e = threadIdx.x; e < G::ZTSZ; e += G::NT) t.zt[e] = a.zt[e];
+  if (t.ncw > 0)
+    for (int e = threadIdx.x; e < G::CORRSZ; e += G::NT) t.corr[e] = a.corrX[e];
+  // tiles with rows next to a y wall: (wall - Toeplitz) column corrections
+  if (t.yedge)
+    for (int e = threadIdx.x; e < G::UR * G::W; e += G::NT) {
+      const int r = e / G::W, k = e - r * G::W;
+      t.yc[2 * e] = a.yT1[(size_t)(t.y0 + r) * G::W + k];
+      t.yc[2 * e + 1] = a.yT3[(size_t)(t.y0 + r) * G::W + k];
+    }
+#if defined(GDM_EXP_ONLYCONS)
+  if (t.wv >= NP) consumer8<P, R, NC, NP, BK, PF, ZI>(a, t);
+#elif defined(GDM_EXP_ONLYPROD)
+  if (t.wv < NP) producer8<P, R, NC, NP, BK, CH>(a, t);
+#else
+  if (t.wv < NP)
+    producer8<P, R, NC, NP, BK, CH>(a, t);
+  else
+    consumer8<P, R, NC, NP, BK, PF, ZI>(a, t);
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // Exact Kronecker mass inverse: banded Cholesky solves along one direction.
 // One thread per line; the position along the line is wave-uniform, so the
@@ -690,20 +1251,107 @@ static hipError_t launch7_p(int bk, const StencilArgs &a, hipStream_t st) {
   }
 }
 
+template <int P, int R, int NC, int NP, int BK, int CH, int PF, bool ZI>
+static hipError_t launch8_t(const StencilArgs &a, hipStream_t st) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget");
+  const size_t lds = G::lds_bytes();
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void *)stencil8_kernel<P, R, NC, NP, BK, CH, PF, ZI>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  int nz = 0;
+  for (int r = 0; r < 2; ++r)
+    if (a.cz1[r] > a.cz0[r]) nz += (a.cz1[r] - a.cz0[r] + a.zchunk - 1) / a.zchunk;
+  dim3 grid((a.Nx + G::TX - 1) / G::TX, (a.out_y1 - a.out_y0 + G::TY - 1) / G::TY, nz);
+  if (grid.x == 0 || grid.y == 0 || grid.z == 0) return hipSuccess;
+  hipLaunchKernelGGL((stencil8_kernel<P, R, NC, NP, BK, CH, PF, ZI>), grid, dim3(G::NT), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int P, int R, int NC, int NP, int PF, bool ZI>
+static hipError_t launch8_z(int bk, const StencilArgs &a, hipStream_t st) {
+  const bool vec = (a.Nx % 2 == 0) && ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0);
+  switch (bk) {
+#ifdef GDM_ONLY_ADV16  // fast experiment builds: advection, 16-B DMA only
+    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF, ZI>(a, st) : hipErrorInvalidValue;
+#else
+    case 0: return vec ? launch8_t<P, R, NC, NP, 0, 16, PF, ZI>(a, st) : launch8_t<P, R, NC, NP, 0, 4, PF, ZI>(a, st);
+    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF, ZI>(a, st) : launch8_t<P, R, NC, NP, 1, 4, PF, ZI>(a, st);
+    case 2: return vec ? launch8_t<P, R, NC, NP, 2, 16, PF, ZI>(a, st) : launch8_t<P, R, NC, NP, 2, 4, PF, ZI>(a, st);
+#endif
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int P, int R, int NC, int NP, int PF>
+static hipError_t launch8_p(int bk, bool zint, const StencilArgs &a, hipStream_t st) {
+  return zint ? launch8_z<P, R, NC, NP, PF, true>(bk, a, st) : launch8_z<P, R, NC, NP, PF, false>(bk, a, st);
+}
+
 }  // namespace gdmk
+
+extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, bool zint, const gdmk::StencilArgs &a, hipStream_t st) {
+  using namespace gdmk;
+  switch (p) {
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 1
+    case 1: return launch8_p<1, 4, 8, 8, 3>(bk, zint, a, st);
+#endif
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 3
+    case 3: return launch8_p<3, 4, 8, 8, 3>(bk, zint, a, st);
+#endif
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 5
+    case 5: return launch8_p<5, GDM_R5, GDM_NC5, GDM_NP5, GDM_PF5>(bk, zint, a, st);
+#endif
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 7
+    case 7: return launch8_p<7, 2, 8, 8, 3>(bk, zint, a, st);
+#endif
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 9
+    case 9: return launch8_p<9, 2, 8, 8, 3>(bk, zint, a, st);
+#endif
+    
+    default: return hipErrorInvalidValue;
+  }
+}
 
 // <P, R, NC, NP>: R output rows per consumer wave, NC consumer and NP producer
 // waves -> tile 64 x (R NC)
 extern "C" int gdmk_stencil_tile_rows(int p) { return p <= 5 ? 32 : 16; }
 
+extern "C" void gdmk_stencil8_geom(int p, int *tile_rows, int *wgs_per_cu) {
+  using namespace gdmk;
+  switch (p) {
+    case 5:
+      *tile_rows = Geom8<5, GDM_R5, GDM_NC5, GDM_NP5, 1>::TY;
+      *wgs_per_cu = Geom8<5, GDM_R5, GDM_NC5, GDM_NP5, 1>::WGS;
+      return;
+    case 7: case 9: *tile_rows = 16; *wgs_per_cu = 1; return;
+    default: *tile_rows = 32; *wgs_per_cu = 1; return;
+  }
+}
+
 extern "C" hipError_t gdmk_launch_stencil(int p, int bk, const gdmk::StencilArgs &a, hipStream_t st) {
   using namespace gdmk;
   switch (p) {
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 1
     case 1: return launch7_p<1, 4, 8, 8>(bk, a, st);
+#endif
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 3
     case 3: return launch7_p<3, 4, 8, 8>(bk, a, st);
+#endif
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 5
     case 5: return launch7_p<5, 4, 8, 8>(bk, a, st);
+#endif
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 7
     case 7: return launch7_p<7, 2, 8, 8>(bk, a, st);
+#endif
+#if !defined(GDM_ONLY_P) || GDM_ONLY_P == 9
     case 9: return launch7_p<9, 2, 8, 8>(bk, a, st);
+#endif
+    
     default: return hipErrorInvalidValue;
   }
 }

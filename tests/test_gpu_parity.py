@@ -148,7 +148,7 @@ def test_mass_solve_vs_cg(dim, p, n):
     assert rel(host(x), x_ref) < RTOL_SOLVE
 
 
-@pytest.mark.parametrize("shape", [(70, 33, 20), (64, 64, 64), (131, 5, 9), (5, 5, 100)])
+@pytest.mark.parametrize("shape", [(70, 33, 20), (64, 64, 64), (131, 5, 9), (5, 5, 100), (150, 90, 70), (97, 61, 130)])
 @pytest.mark.parametrize("p", [5, 7])
 def test_ragged_3d_vs_kron(shape, p):
     """Ragged / non-multiple-of-tile sizes against the Kronecker oracle."""
@@ -164,6 +164,51 @@ def test_ragged_3d_vs_kron(shape, p):
     y = op.new_vector(local=False)
     op.apply(dev(u), y)
     assert rel(host(y), ref) < RTOL_APPLY
+
+
+@pytest.mark.parametrize("kind", ["mass", "wave"])
+@pytest.mark.parametrize("p", [5, 7])
+def test_stencil_walls_3d_vs_kron(kind, p):
+    """Shapes large enough for the v8 stencil (wall rows handled by
+    corrections, interior-z split): mass and wave (+ Nitsche) vs Kronecker."""
+    g = _gdm()
+    n = (130, 75, 66)
+    op = g.GdmOperator(3, p, n, (-1.0, 0.0, 0.5), (1.2, 0.9, 1.4), kind)
+    m = O.Mesh(3, p, n, (-1.0, 0.0, 0.5), (1.2, 0.9, 1.4))
+    u = np.random.default_rng(9).uniform(-1, 1, m.n_dofs)
+    M = [m.matrices_1d(d)[0] for d in range(3)]
+    if kind == "mass":
+        terms = [(M[0], M[1], M[2])]
+    else:
+        B = [-m.matrices_1d(d)[2] for d in range(3)]
+        terms = [(B[0], M[1], M[2]), (M[0], B[1], M[2]), (M[0], M[1], B[2])]
+    ref = m.kron_apply(terms, u)
+    y = op.new_vector(local=False)
+    op.apply(dev(u), y)
+    assert rel(host(y), ref) < RTOL_APPLY
+
+
+@pytest.mark.parametrize("p", [5, 7])
+def test_stencil_walls_2d_vs_cell_loop(p):
+    """2D meshes large enough for the v8 stencil: wave with box Nitsche
+    (rank-2 wall-row terms) and advection with inflow data vs the cell loops."""
+    g = _gdm()
+    n = (80, 50)
+    m = O.Mesh(2, p, list(n), -1.21, 1.21)
+    rng = np.random.default_rng(10)
+    u = rng.uniform(-1, 1, m.n_dofs)
+    op = g.GdmOperator(2, p, n, -1.21, 1.21, "wave", params=(15.0,))
+    y = op.new_vector(local=False)
+    op.apply(dev(u), y)
+    assert rel(host(y), m.wave_rhs(u, impl=True, nitsche=15.0)) < RTOL_APPLY
+    a = (-0.6, 0.9)
+    op = g.GdmOperator(2, p, n, -1.21, 1.21, "advection", params=a)
+    bc_ref = rng.uniform(-1, 1, m.n_boundary_points())
+    bc_dev = np.zeros_like(bc_ref)
+    bc_dev[op.bc_reference_order()] = bc_ref
+    y = op.new_vector(local=False)
+    op.apply(dev(u), y, dev(bc_dev))
+    assert rel(host(y), m.advection_rhs(a, u, bc_ref)) < RTOL_APPLY
 
 
 def test_full_size_properties_3d_p5():
