@@ -1,0 +1,368 @@
+// gdm/hip/operators.h -- C++ host mirror of the reference's operator surface
+// over the C ABI of libgdm_hip.so (include/gdm_hip.h).
+//
+// Same class and method names, argument meaning and error behaviour as the
+// reference (paths relative to peterrum/dealii-galerkin-difference-methods):
+//   Parameters<dim>              applications/advection/include/gdm/advection/parameters.h:5-47
+//   Discretization<dim>          .../advection/discretization.h:21-177
+//   StiffnessMatrixOperator<dim> .../advection/stiffness.h:18-606
+//     initialize_dof_vector      :162-179   (block(0) = boundary points, block(1) = solution)
+//     initialize_time_step       :181-194   (block(0) <- g(t_n))
+//     compute_rhs                :196-606   (block(0) = dg/dt, block(1) = K u + inflow data)
+//   MassMatrixOperator<dim>      .../advection/mass.h:18-243 (vmult on the matrix-free mass)
+//   AdvectionProblem<dim>        .../advection/problem.h:13-205 (RK4 + DiscreteTime + solve)
+// deal.II is not needed: vectors are device buffers owned by DeviceVector, the
+// mesh is the uncut subdivided hyper cube, the advection field is constant and
+// the level set cuts nothing (the uncut configuration of BASELINE.json).
+// Errors: every ABI failure throws GDM::HIP::Error (the reference's
+// AssertThrow); there is no CPU fallback.
+#pragma once
+
+#include <gdm_hip.h>
+
+#include <array>
+#include <cmath>
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace GDM {
+namespace HIP {
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+inline void check(int rc, const char *what) {
+  if (rc != GDM_OK) {
+    char buf[1024];
+    gdm_last_error(buf, sizeof(buf));
+    throw Error(std::string(what) + ": " + buf);
+  }
+}
+
+using Point = std::array<double, 3>;
+using Function = std::function<double(const Point &, double)>;  // (x, t) -> value
+
+// applications/advection/include/gdm/advection/parameters.h (uncut subset)
+template <int dim>
+struct Parameters {
+  unsigned int fe_degree = 5;
+  unsigned int n_subdivisions_1D = 40;
+  double geometry_left = 0.0;
+  double geometry_right = 1.0;
+  Function exact_solution;      // g(x, t): initial condition and inflow data
+  Function exact_solution_der;  // dg/dt(x, t): evolves block(0) (stiffness.h:286-289)
+  double start_t = 0.0;
+  double end_t = 0.1;
+  double cfl = 0.1;
+  double max_val = 1.0;                 // max |a| for the time step (problem.h:45)
+  std::array<double, dim> advection{};  // constant field a
+  int device = 0;
+  int n_ranks = 1, rank = 0;            // z-slab partition (system.h:720-757)
+};
+
+// A device buffer of doubles allocated through the engine (gdm_malloc).
+class DeviceVector {
+ public:
+  DeviceVector() = default;
+  DeviceVector(gdm_op *op, std::size_t n) { reinit(op, n); }
+  DeviceVector(const DeviceVector &) = delete;
+  DeviceVector &operator=(const DeviceVector &) = delete;
+  DeviceVector(DeviceVector &&o) noexcept { swap(o); }
+  DeviceVector &operator=(DeviceVector &&o) noexcept {
+    swap(o);
+    return *this;
+  }
+  ~DeviceVector() {
+    if (ptr_) gdm_free(op_, ptr_);
+  }
+  void reinit(gdm_op *op, std::size_t n) {
+    if (ptr_) gdm_free(op_, ptr_);
+    op_ = op;
+    n_ = n;
+    void *p = nullptr;
+    check(gdm_malloc(op_, sizeof(double) * std::max<std::size_t>(n, 1), &p), "gdm_malloc");
+    ptr_ = static_cast<double *>(p);
+    *this = 0.0;
+  }
+  DeviceVector &operator=(double s) {  // only 0 is meaningful, like deal.II
+    if (n_) check(gdm_vec_axpby(op_, (int64_t)n_, 0.0, ptr_, 0.0, ptr_), "gdm_vec_axpby");
+    (void)s;
+    return *this;
+  }
+  void upload(const std::vector<double> &h) {
+    if (h.size() != n_) throw Error("DeviceVector::upload: size mismatch");
+    if (n_) check(gdm_memcpy_h2d(op_, ptr_, h.data(), sizeof(double) * n_), "gdm_memcpy_h2d");
+  }
+  std::vector<double> download() const {
+    std::vector<double> h(n_);
+    if (n_) check(gdm_memcpy_d2h(op_, h.data(), ptr_, sizeof(double) * n_), "gdm_memcpy_d2h");
+    return h;
+  }
+  // this = a x + b this
+  void sadd(double b, double a, const DeviceVector &x) {
+    if (x.n_ != n_) throw Error("DeviceVector::sadd: size mismatch");
+    if (n_) check(gdm_vec_axpby(op_, (int64_t)n_, a, x.ptr_, b, ptr_), "gdm_vec_axpby");
+  }
+  double operator*(const DeviceVector &x) const {
+    double r = 0.0;
+    check(gdm_vec_dot(op_, (int64_t)n_, ptr_, x.ptr_, &r), "gdm_vec_dot");
+    return r;
+  }
+  std::size_t size() const { return n_; }
+  double *get_values() { return ptr_; }
+  const double *get_values() const { return ptr_; }
+
+ private:
+  void swap(DeviceVector &o) noexcept {
+    std::swap(op_, o.op_);
+    std::swap(ptr_, o.ptr_);
+    std::swap(n_, o.n_);
+  }
+  gdm_op *op_ = nullptr;
+  double *ptr_ = nullptr;
+  std::size_t n_ = 0;
+};
+
+// LinearAlgebra::distributed::BlockVector with the two blocks the advection
+// operator uses: block(0) = stage boundary values, block(1) = DoF values in the
+// local layout [ghost planes | owned planes | ghost planes].
+struct BlockVector {
+  DeviceVector b0, b1;
+  DeviceVector &block(unsigned int i) { return i == 0 ? b0 : b1; }
+  const DeviceVector &block(unsigned int i) const { return i == 0 ? b0 : b1; }
+  void sadd(double b, double a, const BlockVector &x) {
+    b0.sadd(b, a, x.b0);
+    b1.sadd(b, a, x.b1);
+  }
+};
+
+// .../advection/discretization.h: the mesh, categories and partition (held by
+// the engine) plus the quantities the problem driver reads.
+template <int dim>
+class Discretization {
+ public:
+  void reinit(const Parameters<dim> &params) {
+    desc = gdm_mesh_desc{};
+    desc.dim = dim;
+    desc.fe_degree = (int)params.fe_degree;
+    for (int d = 0; d < 3; ++d) {
+      desc.n_subdivisions[d] = d < dim ? (int)params.n_subdivisions_1D : 1;
+      desc.lo[d] = d < dim ? params.geometry_left : 0.0;
+      desc.hi[d] = d < dim ? params.geometry_right : 1.0;
+    }
+    desc.n_ranks = params.n_ranks;
+    desc.rank = params.rank;
+    device = params.device;
+  }
+  double get_dx() const { return (desc.hi[0] - desc.lo[0]) / desc.n_subdivisions[0]; }  // discretization.h:50
+  const gdm_mesh_desc &get_mesh() const { return desc; }
+  int get_device() const { return device; }
+
+ private:
+  gdm_mesh_desc desc{};
+  int device = 0;
+};
+
+template <int dim>
+class StiffnessMatrixOperator {
+ public:
+  explicit StiffnessMatrixOperator(const Discretization<dim> &discretization) : discretization(discretization) {}
+  StiffnessMatrixOperator(const StiffnessMatrixOperator &) = delete;
+  ~StiffnessMatrixOperator() { gdm_op_destroy(op); }
+
+  void reinit(const Parameters<dim> &params) {
+    gdm_op_destroy(op);
+    op = nullptr;
+    check(gdm_op_create(&discretization.get_mesh(), GDM_OP_ADVECTION, params.advection.data(), dim,
+                        discretization.get_device(), &op),
+          "gdm_op_create");
+    check(gdm_op_layout(op, &layout), "gdm_op_layout");
+    // every operator of a problem launches on the HIP null stream, so calls on
+    // different operators stay ordered like the reference's serial calls
+    check(gdm_op_set_stream(op, nullptr), "gdm_op_set_stream");
+    exact_solution = params.exact_solution;
+    exact_solution_der = params.exact_solution_der;
+    // boundary points of the owned cells (device order), collect_boundary_points (:40-160)
+    std::vector<double> xyz(3 * std::max<int64_t>(layout.n_bc_points, 1));
+    check(gdm_bc_points(op, xyz.data()), "gdm_bc_points");
+    all_points_0.resize(layout.n_bc_points);
+    for (int64_t i = 0; i < layout.n_bc_points; ++i) all_points_0[i] = {xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]};
+  }
+
+  void initialize_dof_vector(BlockVector &vec) const {
+    vec.b0.reinit(op, layout.n_bc_points);
+    vec.b1.reinit(op, layout.n_local);
+  }
+
+  void initialize_time_step(BlockVector &stage_bc_and_solution, const double time) const {
+    stage_bc_and_solution.block(0).upload(evaluate(exact_solution, time));
+  }
+
+  // vec_rhs.block(1) (owned entries of its local layout) = K u + inflow
+  // data; vec_rhs.block(0) = dg/dt at the boundary points.  The ghost planes of
+  // src.block(1) must be current (update_ghost_values, stiffness.h:343).
+  void compute_rhs(BlockVector &vec_rhs, const BlockVector &stage_bc_and_solution, const double time) const {
+    vec_rhs.block(0).upload(evaluate(exact_solution_der, time));
+    check(gdm_apply(op, stage_bc_and_solution.block(1).get_values(), owned(vec_rhs.block(1)),
+                    stage_bc_and_solution.block(0).get_values()),
+          "gdm_apply");
+  }
+
+  gdm_op *handle() const { return op; }
+  const gdm_layout &get_layout() const { return layout; }
+  double *owned(DeviceVector &v) const { return v.get_values() + layout.ghost_planes_below * layout.plane_size; }
+  const double *owned(const DeviceVector &v) const {
+    return v.get_values() + layout.ghost_planes_below * layout.plane_size;
+  }
+
+ private:
+  std::vector<double> evaluate(const Function &f, double t) const {
+    std::vector<double> v(all_points_0.size());
+    for (std::size_t i = 0; i < v.size(); ++i) v[i] = f ? f(all_points_0[i], t) : 0.0;
+    return v;
+  }
+  const Discretization<dim> &discretization;
+  gdm_op *op = nullptr;
+  gdm_layout layout{};
+  Function exact_solution, exact_solution_der;
+  std::vector<Point> all_points_0;
+};
+
+// .../advection/mass.h: the matrix-free mass operator models deal.II's
+// MatrixType (vmult); solve() replaces the CG + ILU solve of problem.h:236-267
+// by the exact Kronecker inverse.
+template <int dim>
+class MassMatrixOperator {
+ public:
+  explicit MassMatrixOperator(const Discretization<dim> &discretization) : discretization(discretization) {}
+  MassMatrixOperator(const MassMatrixOperator &) = delete;
+  ~MassMatrixOperator() { gdm_op_destroy(op); }
+  void reinit(const Parameters<dim> &) {
+    gdm_op_destroy(op);
+    op = nullptr;
+    check(gdm_op_create(&discretization.get_mesh(), GDM_OP_MASS, nullptr, 0, discretization.get_device(), &op),
+          "gdm_op_create");
+    check(gdm_op_layout(op, &layout), "gdm_op_layout");
+    check(gdm_op_set_stream(op, nullptr), "gdm_op_set_stream");  // ordered with the stiffness operator
+  }
+  // dst (owned) = M src (local layout, ghosts current)
+  void vmult(double *dst_owned, const double *src_local) const { check(gdm_mass_apply(op, src_local, dst_owned), "gdm_mass_apply"); }
+  // x = M^-1 rhs (owned vectors)
+  void solve(double *x_owned, const double *rhs_owned) const { check(gdm_mass_solve(op, rhs_owned, x_owned), "gdm_mass_solve"); }
+  gdm_op *handle() const { return op; }
+
+ private:
+  const Discretization<dim> &discretization;
+  gdm_op *op = nullptr;
+  gdm_layout layout{};
+};
+
+// deal.II DiscreteTime: fixed steps, the last one shrunk to hit end_t or, when
+// the remainder would be tiny, the previous one stretched.
+class DiscreteTime {
+ public:
+  DiscreteTime(double start, double end, double dt) : t(start), end(end), dt(dt) {}
+  bool is_at_end() const { return !(t < end); }
+  double get_current_time() const { return t; }
+  double get_next_step_size() const {
+    if (t + dt >= end || t + 1.05 * dt > end) return end - t;
+    return dt;
+  }
+  void advance_time() {
+    const double h = get_next_step_size();
+    t = (t + h >= end) ? end : t + h;
+    ++steps;
+  }
+  unsigned int get_step_number() const { return steps; }
+
+ private:
+  double t, end, dt;
+  unsigned int steps = 0;
+};
+
+// .../advection/problem.h:31-102 (non-composite branch): explicit RK4
+// (RK_CLASSIC_FOURTH_ORDER) on (block(0), block(1)) with
+// f(t, y) = (dg/dt, M^-1 (K u + inflow data)).
+template <int dim>
+class AdvectionProblem {
+ public:
+  explicit AdvectionProblem(const Parameters<dim> &params)
+      : params(params), mass_matrix_operator(discretization), stiffness_matrix_operator(discretization) {}
+
+  // Runs to end_t (or max_steps); returns the number of steps.  The solution
+  // is available through get_solution() (owned DoFs, reference global order).
+  unsigned int run(unsigned int max_steps = ~0u) {
+    if (params.n_ranks != 1) throw Error("AdvectionProblem: the host RK driver is single-rank");
+    discretization.reinit(params);
+    mass_matrix_operator.reinit(params);
+    stiffness_matrix_operator.reinit(params);
+    const double delta_t = discretization.get_dx() * params.cfl / params.max_val;  // problem.h:45
+    stiffness_matrix_operator.initialize_dof_vector(solution);
+    set_initial_condition(solution.block(1));
+    BlockVector k[4], stage;
+    for (auto &v : k) stiffness_matrix_operator.initialize_dof_vector(v);
+    stiffness_matrix_operator.initialize_dof_vector(stage);
+    const auto fu_rhs = [&](double time, const BlockVector &y, BlockVector &result) {
+      stiffness_matrix_operator.compute_rhs(result, y, time);
+      double *r = stiffness_matrix_operator.owned(result.block(1));
+      mass_matrix_operator.solve(r, r);
+    };
+    DiscreteTime time(params.start_t, params.end_t, delta_t);
+    static const double c[4] = {0.0, 0.5, 0.5, 1.0}, aa[4] = {0.0, 0.5, 0.5, 1.0},
+                        b[4] = {1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0};
+    unsigned int n = 0;
+    while (!time.is_at_end() && n < max_steps) {
+      stiffness_matrix_operator.initialize_time_step(solution, time.get_current_time());  // evaluate bc
+      const double t0 = time.get_current_time(), h = time.get_next_step_size();
+      for (int s = 0; s < 4; ++s) {
+        // Y_s = y + h a_s k_{s-1}
+        stage.sadd(0.0, 1.0, solution);
+        if (s > 0) stage.sadd(1.0, h * aa[s], k[s - 1]);
+        fu_rhs(t0 + c[s] * h, s == 0 ? solution : stage, k[s]);
+      }
+      for (int s = 0; s < 4; ++s) solution.sadd(1.0, h * b[s], k[s]);
+      time.advance_time();
+      ++n;
+    }
+    return n;
+  }
+
+  std::vector<double> get_solution() const { return solution.block(1).download(); }
+  const BlockVector &get_solution_vector() const { return solution; }
+
+ private:
+  // VectorTools::interpolate of the GDM vertex basis = vertex values (vector_tools.h:11-23)
+  void set_initial_condition(DeviceVector &u) const {
+    const gdm_mesh_desc &m = discretization.get_mesh();
+    const gdm_layout &L = stiffness_matrix_operator.get_layout();
+    std::vector<double> h(L.n_local);
+    const int N0 = m.n_subdivisions[0] + 1, N1 = dim > 1 ? m.n_subdivisions[1] + 1 : 1;
+    const int64_t first_plane = L.owned_plane_begin - L.ghost_planes_below;
+    for (int64_t i = 0; i < L.n_local; ++i) {
+      const int64_t g = first_plane * L.plane_size + i;  // global lexicographic index
+      Point x{0.0, 0.0, 0.0};
+      int64_t r = g;
+      const int64_t n[3] = {N0, N1, 0};
+      for (int d = 0; d < dim; ++d) {
+        const int64_t id = d + 1 < dim ? r % n[d] : r;
+        if (d + 1 < dim) r /= n[d];
+        x[d] = m.lo[d] + id * (m.hi[d] - m.lo[d]) / m.n_subdivisions[d];
+      }
+      h[i] = params.exact_solution(x, params.start_t);
+    }
+    u.upload(h);
+  }
+
+  Parameters<dim> params;
+  Discretization<dim> discretization;
+  MassMatrixOperator<dim> mass_matrix_operator;
+  StiffnessMatrixOperator<dim> stiffness_matrix_operator;
+  BlockVector solution;
+};
+
+}  // namespace HIP
+}  // namespace GDM
