@@ -418,10 +418,20 @@ void build_faces(gdm_op *op) {
       unsigned cb = 0, ce = nce;
       int nb = 0, ne = op->N[e];
       if (e == q) {
-        cb = (unsigned)L.cell_plane_begin;
-        ce = (unsigned)L.cell_plane_end;
+        // owner-computes: every cell whose DoF box reaches an owned node, the
+        // neighbour ranks' cells included (their points are ghost points)
         nb = L.owned_plane_begin;
         ne = L.owned_plane_end;
+        cb = nce;
+        ce = 0;
+        for (unsigned c = 0; c < nce; ++c) {
+          const int off = (int)gdm::box_offset(c, p, nce);
+          if (off + p >= nb && off <= ne - 1) {
+            cb = std::min(cb, c);
+            ce = std::max(ce, c + 1);
+          }
+        }
+        if (ce <= cb) cb = ce = (unsigned)L.cell_plane_begin;
       }
       gdm::FaceTable ft = gdm::face_table_1d(p, nce, h, cb, ce);
       t.n_nodes = op->N[e];
@@ -457,6 +467,24 @@ void build_faces(gdm_op *op) {
     op->faces.push_back(F);
   }
   op->layout.n_bc_points = offset;
+  // the reference's block(0): points of the owned cells only
+  {
+    int64_t nref = 0;
+    const int n1q = p + 1;
+    const int nfq = dim == 1 ? 1 : (dim == 2 ? n1q : n1q * n1q);
+    int ncell[3] = {1, 1, 1};
+    for (int d = 0; d < dim; ++d) ncell[d] = op->mesh.n_subdivisions[d];
+    for (const Face &F : op->faces) {
+      // owned cells adjacent to face F: product of the tangential owned cell counts
+      int64_t cells = 1;
+      for (int e = 0; e < dim; ++e) {
+        if (e == F.d) continue;
+        cells *= e == q ? (L.cell_plane_end - L.cell_plane_begin) : ncell[e];
+      }
+      nref += cells * nfq;
+    }
+    op->layout.n_bc_points_ref = nref;
+  }
   op->face_tmp_size = max_tmp;
   hip_check(hipMalloc(&op->face_tmp, sizeof(double) * max_tmp), "hipMalloc");
   keep(op, op->face_tmp);
@@ -902,7 +930,7 @@ int gdm_bc_reference_order(const gdm_op *op, int64_t *ref_to_dev_host) {
           }
         }
       }
-  if (k != L.n_bc_points) return fail(GDM_ERR_STATE, "boundary point count mismatch");
+  if (k != L.n_bc_points_ref) return fail(GDM_ERR_STATE, "boundary point count mismatch");
   return GDM_OK;
 }
 

@@ -49,6 +49,7 @@ class Layout(ctypes.Structure):
         ("n_owned", ctypes.c_int64),
         ("n_local", ctypes.c_int64),
         ("n_bc_points", ctypes.c_int64),
+        ("n_bc_points_ref", ctypes.c_int64),
     ]
 
     def as_dict(self):

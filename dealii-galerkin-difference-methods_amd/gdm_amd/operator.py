@@ -164,8 +164,12 @@ class GdmOperator:
         check(self.lib.gdm_bc_points(self.h, xyz.ctypes.data_as(ctypes.c_void_p)), "gdm_bc_points")
         return xyz[:n]
 
+    @property
+    def n_bc_points_ref(self):
+        return self.layout["n_bc_points_ref"]
+
     def bc_reference_order(self):
-        n = self.n_bc_points
+        n = self.n_bc_points_ref
         perm = np.zeros(max(n, 1), dtype=np.int64)
         check(self.lib.gdm_bc_reference_order(self.h, perm.ctypes.data_as(ctypes.c_void_p)),
               "gdm_bc_reference_order")

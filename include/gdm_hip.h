@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 1
+#define GDM_HIP_ABI_VERSION 2
 
 enum gdm_status {
   GDM_OK = 0,
@@ -104,7 +104,12 @@ typedef struct {
   int32_t halo_depth;             /* = fe_degree                                */
   int64_t n_owned;                /* owned DoFs                                 */
   int64_t n_local;                /* owned + ghost DoFs                         */
-  int64_t n_bc_points;            /* block(0) size (boundary points of owned cells) */
+  int64_t n_bc_points;            /* device block(0) size: boundary points of the owned
+                                     cells plus, on a multi-rank mesh, those of the
+                                     neighbour cells whose DoF boxes reach owned DoFs
+                                     (owner-computes replaces compress(add)) */
+  int64_t n_bc_points_ref;        /* the reference's block(0) size: points of the owned
+                                     cells only (stiffness.h:40-160)                  */
 } gdm_layout;
 
 /* params (n_params):
@@ -150,9 +155,11 @@ int gdm_free(gdm_op *op, void *ptr);
 int gdm_memcpy_h2d(gdm_op *op, void *dst, const void *src_host, size_t bytes);
 int gdm_memcpy_d2h(gdm_op *op, void *dst_host, const void *src, size_t bytes);
 
-/* boundary points of the owned cells: coordinates (n_bc_points x 3, device
- * order) and ref_to_dev[i] = device index of the i-th point in the
- * reference's block(0) order (cells lexicographic, faces 0..2dim-1, q). */
+/* boundary points: coordinates of all n_bc_points device points (device
+ * order; the caller evaluates its boundary data there, ghost-cell points
+ * included) and ref_to_dev[i] = device index of the i-th point in the
+ * reference's block(0) order (owned cells lexicographic, faces 0..2dim-1, q;
+ * n_bc_points_ref entries). */
 int gdm_bc_points(const gdm_op *op, double *xyz_host);
 int gdm_bc_reference_order(const gdm_op *op, int64_t *ref_to_dev_host);
 

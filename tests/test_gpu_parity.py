@@ -249,7 +249,9 @@ def test_slab_ranks_match_single_rank(n_ranks, shape, p, kind):
     process: each rank's operator on its [ghost | owned | ghost] local vector,
     ghosts filled from the global vector exactly as HaloExchange does, must
     reproduce the single-rank result on the owned planes (bit-identical DoF
-    numbering, fp64 tolerance for the values)."""
+    numbering, fp64 tolerance for the values).  Advection includes the inflow
+    data of the x/y faces, whose owned nodes near a slab edge also collect the
+    neighbour cells' boundary points (owner-computes instead of compress(add))."""
     g = _gdm()
     from gdm_amd.distributed import layout as slab_layout
 
@@ -258,8 +260,14 @@ def test_slab_ranks_match_single_rank(n_ranks, shape, p, kind):
     lo, hi = (0.0, -0.5, 0.2), (1.0, 0.5, 1.7)
     full = g.GdmOperator(3, p, shape, lo, hi, kind, params=params)
     u = torch.rand(full.n_owned, dtype=torch.float64, device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+    def bc_for(op):  # smooth inflow data at the operator's device boundary points (ghost-cell points included)
+        if kind != "advection":
+            return None
+        x = op.bc_points()
+        return dev(np.sin(3 * x[:, 0] + 1) * np.cos(2 * x[:, 1] - 0.5) + x[:, 2])
+
     ref = full.new_vector(local=False)
-    full.apply(u, ref)
+    full.apply(u, ref, bc_for(full))
     ps = full.layout["plane_size"]
     out = torch.zeros_like(ref)
     for r in range(n_ranks):
@@ -269,7 +277,8 @@ def test_slab_ranks_match_single_rank(n_ranks, shape, p, kind):
         first = L["owned_plane_begin"] - L["ghost_planes_below"]
         local = u[first * ps:first * ps + L["n_local"]].clone()
         y = op.new_vector(local=False)
-        op.apply(local, y)
+        op.apply(local, y, bc_for(op))
+        assert op.n_bc_points_ref <= op.n_bc_points
         b = L["owned_plane_begin"] * ps
         out[b:b + L["n_owned"]] = y
     torch.cuda.synchronize()
