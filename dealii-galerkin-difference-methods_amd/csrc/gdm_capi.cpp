@@ -802,6 +802,25 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
   GDM_GUARD_END
 }
 
+int gdm_mass_solve_lines(gdm_op *op, int axis, double *v, int64_t n_lines, int64_t stride, int64_t A, int64_t B,
+                         int64_t C) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (axis < 0 || axis >= op->dim) return fail(GDM_ERR_ARG, "axis out of range");
+  if (n_lines < 0 || stride <= 0 || A <= 0) return fail(GDM_ERR_ARG, "bad line geometry");
+  if (n_lines > 0 && !v) return fail(GDM_ERR_ARG, "NULL vector");
+  int kax = -1;
+  for (int ax = 0; ax < 3; ++ax)
+    if (op->kdir[ax] == axis) kax = ax;
+  if (kax < 0 || !op->lrow[kax]) return n_lines == 0 || op->N[axis] <= 1 ? GDM_OK : fail(GDM_ERR_STATE, "no factor");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  hip_check(gdmk_launch_chol_lines(op->p, v, op->N[axis], stride, n_lines, A, B, C, op->lrow[kax], op->invd[kax],
+                                   op->stream),
+            "chol lines");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
 int gdm_vec_axpby(gdm_op *op, int64_t n, double a, const double *x, double b, double *y) {
   if (!op || (n > 0 && (!x || !y))) return fail(GDM_ERR_ARG, "NULL argument");
   GDM_GUARD_BEGIN

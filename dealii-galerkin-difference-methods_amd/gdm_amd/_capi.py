@@ -81,6 +81,7 @@ def load():
         "gdm_add_boundary_data": [P, P, P],
         "gdm_mass_apply": [P, P, P],
         "gdm_mass_solve": [P, P, P],
+        "gdm_mass_solve_lines": [P, i32, P, i64, i64, i64, i64, i64],
         "gdm_vec_axpby": [P, i64, d, P, d, P],
         "gdm_vec_dot": [P, i64, P, P, ctypes.POINTER(d)],
         "gdm_synchronize": [P],

@@ -95,3 +95,113 @@ class HaloExchange:
     def exchange(self, local):
         self.finish(self.start(local))
         return local
+
+
+def chunks(n, n_ranks):
+    """Contiguous split of n items over n_ranks: [(begin, end)] per rank."""
+    base, extra = divmod(n, n_ranks)
+    out, b = [], 0
+    for r in range(n_ranks):
+        e = b + base + (1 if r < extra else 0)
+        out.append((b, e))
+        b = e
+    return out
+
+
+class DistributedMassSolve:
+    """x = M^-1 r on a slab-partitioned mesh (replaces the CG + ILU/AMG solve of
+    applications/advection/include/gdm/advection/problem.h:236-267 and
+    applications/wave/include/gdm/wave/problem.h:457-502 across ranks).
+
+    M^-1 = M_q^-1 (x) ... (x) M_0^-1 exactly (Kronecker form of the uncut mass
+    matrix).  The directions inside a slab are solved in place; the
+    partitioned direction q = dim - 1 is solved after a transpose: every rank
+    sends the part of its owned planes that falls into each rank's chunk of
+    the plane (contiguous entries of the lexicographic plane), so rank s ends
+    up with all N_q planes of its chunk, solves those lines, and the inverse
+    transpose restores the slab layout.  Point-to-point only (RCCL over xGMI
+    for device tensors, gloo for the CPU tests).
+
+    line_solve(axis, v, n_lines, stride, A, B, C) solves in place along
+    `axis`; default: the operator's gdm_mass_solve_lines."""
+
+    def __init__(self, dim, n_vertices, n_ranks, rank, op=None, line_solve=None, group=None):
+        self.dim, self.N = dim, list(n_vertices) + [1] * (3 - dim)
+        self.n_ranks, self.rank, self.group = n_ranks, rank, group
+        q = dim - 1
+        self.plane = 1
+        for d in range(q):
+            self.plane *= self.N[d]
+        self.lays = [layout(self.N[q] - 1, n_ranks, r, self.plane, 0) for r in range(n_ranks)]
+        self.chunk = chunks(self.plane, n_ranks)
+        self.solve_lines = line_solve or (lambda *a: op.mass_solve_lines(*a))
+
+    def _planes(self, r):
+        L = self.lays[r]
+        return L["owned_plane_end"] - L["owned_plane_begin"]
+
+    def _local(self, x):
+        """In-place solves along the directions inside the slab."""
+        Nx, Ny = self.N[0], self.N[1]
+        npl = self._planes(self.rank)
+        if npl == 0:
+            return
+        if self.dim >= 2:  # x lines
+            n = npl * (Ny if self.dim == 3 else 1)
+            self.solve_lines(0, x, n, 1, n, 0, Nx)
+        if self.dim == 3:  # y lines: (x, plane) -> base = plane * Nx * Ny + x
+            self.solve_lines(1, x, Nx * npl, Nx, Nx, Nx * Ny, 1)
+
+    def _exchange(self, send_of, recv_into):
+        import torch.distributed as dist
+
+        ops = []
+        for s in range(self.n_ranks):
+            if s == self.rank:
+                continue
+            b = send_of(s)
+            if b is not None and b.numel():
+                ops.append(dist.P2POp(dist.isend, b, s, group=self.group))
+            c = recv_into(s)
+            if c is not None and c.numel():
+                ops.append(dist.P2POp(dist.irecv, c, s, group=self.group))
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+
+    def solve(self, rhs_owned, x_owned):
+        import torch
+
+        x = x_owned
+        if x.data_ptr() != rhs_owned.data_ptr():
+            x.copy_(rhs_owned)
+        self._local(x)
+        me, P = self.rank, self.plane
+        c0, c1 = self.chunk[me]
+        w = c1 - c0
+        first = [L["owned_plane_begin"] for L in self.lays]
+        npl = [self._planes(r) for r in range(self.n_ranks)]
+        Nq = self.N[self.dim - 1]
+        x2 = x.view(npl[me], P) if npl[me] else x.view(0, P)
+        # forward transpose: Z[plane, chunk entry] for all planes of my chunk
+        Z = torch.empty((Nq, w), dtype=x.dtype, device=x.device)
+        sendbuf = {s: x2[:, self.chunk[s][0]:self.chunk[s][1]].contiguous() for s in range(self.n_ranks)}
+        recvbuf = {s: torch.empty((npl[s], w), dtype=x.dtype, device=x.device) for s in range(self.n_ranks)}
+        recvbuf[me] = sendbuf[me]
+        self._exchange(lambda s: sendbuf[s], lambda s: recvbuf[s])
+        for s in range(self.n_ranks):
+            if npl[s]:
+                Z[first[s]:first[s] + npl[s]] = recvbuf[s]
+        if w:
+            self.solve_lines(self.dim - 1, Z.view(-1), w, w, w, 0, 1)
+        # inverse transpose
+        back = {s: Z[first[s]:first[s] + npl[s]].contiguous() for s in range(self.n_ranks)}
+        got = {s: torch.empty((npl[me], self.chunk[s][1] - self.chunk[s][0]), dtype=x.dtype, device=x.device)
+               for s in range(self.n_ranks)}
+        got[me] = back[me]
+        self._exchange(lambda s: back[s], lambda s: got[s])
+        for s in range(self.n_ranks):
+            a, b = self.chunk[s]
+            if npl[me] and b > a:
+                x2[:, a:b] = got[s]
+        return x

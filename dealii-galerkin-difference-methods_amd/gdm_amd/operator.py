@@ -139,6 +139,12 @@ class GdmOperator:
         check(self.lib.gdm_mass_solve(self.h, _ptr(rhs_owned), _ptr(x_owned)), "gdm_mass_solve")
         return x_owned
 
+    def mass_solve_lines(self, axis, v, n_lines, stride, A, B, C):
+        """In-place 1D mass solves along `axis` (gdm_mass_solve_lines)."""
+        check(self.lib.gdm_mass_solve_lines(self.h, int(axis), _ptr(v), int(n_lines), int(stride), int(A), int(B),
+                                            int(C)), "gdm_mass_solve_lines")
+        return v
+
     def axpby(self, a, x, b, y):
         check(self.lib.gdm_vec_axpby(self.h, x.numel(), float(a), _ptr(x), float(b), _ptr(y)), "gdm_vec_axpby")
         return y

@@ -144,6 +144,16 @@ int gdm_mass_apply(gdm_op *op, const double *src_local, double *dst_owned);
 /* x_owned = M^-1 rhs_owned (exact Kronecker inverse; single rank) */
 int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned);
 
+/* In-place banded-Cholesky solve with the 1D mass matrix of reference
+ * direction `axis` (0 = x, 1 = y, 2 = z) along n_lines lines of full length
+ * N[axis]: line l starts at v + (l / A) * B + (l % A) * C and its entries are
+ * `stride` apart.  The building block of the distributed mass inverse (the
+ * slab-local directions are solved in place, the partitioned one after a
+ * transpose; gdm_amd/distributed.py), replacing the CG of
+ * advection/problem.h:236-267 on a multi-rank mesh. */
+int gdm_mass_solve_lines(gdm_op *op, int axis, double *v, int64_t n_lines, int64_t stride, int64_t A, int64_t B,
+                         int64_t C);
+
 /* y = a x + b y ; *result_host = x . y */
 int gdm_vec_axpby(gdm_op *op, int64_t n, double a, const double *x, double b, double *y);
 int gdm_vec_dot(gdm_op *op, int64_t n, const double *x, const double *y, double *result_host);
