@@ -533,7 +533,12 @@ struct Geom8 {
   static constexpr int NPASS = (NG + NP - 1) / NP;
   static constexpr int USZ = NG * 4 * RL;
   static constexpr int NAB = BK == 0 ? 1 : 2;
-  static constexpr int ABSZ = UR * TX * NAB;
+  // (A, B) pairs: row stride 2 TX + 2 TX / 8 doubles with one pair of padding
+  // after every 8 x -- the producers' 4-pairs-per-lane ds_write_b128 stores
+  // then hit distinct banks; consumers read one pair per lane as before
+  static constexpr int ABRS = NAB == 2 ? 2 * TX + 2 * (TX / 8) : TX;
+  static constexpr int ABSZ = UR * ABRS;
+  static __device__ __forceinline__ int ab(int r, int x) { return NAB == 2 ? r * ABRS + 2 * x + 2 * (x >> 3) : r * TX + x; }
   static constexpr int ZTSZ = (2 * W + 1) * W * 2;  // wall planes + interior row
   static constexpr int YCSZ = UR * W * 2;
   static constexpr int CORRSZ = 2 * (P + 1) * 2 * W;
@@ -644,7 +649,7 @@ __device__ __forceinline__ void xwall8_calc(const StencilArgs &a, const Tile7 &t
 #pragma unroll
       for (int k = 0; k < W; ++k) d = fma(cm[k], ur[k], d);
       xw.v[it] = d;
-      xw.o[it] = BK != 0 ? (r * TX + lx) * 2 + comp : r * TX + lx;
+      xw.o[it] = G::ab(r, lx) + (BK != 0 ? comp : 0);
     }
   }
 }
@@ -665,7 +670,7 @@ __device__ __forceinline__ void write_ab8(const Tile7 &t, int g, const double (&
   const int r = 4 * g + rr;
   if (r < G::UR) {
     if constexpr (BK != 0) {
-      ldouble2 *p = (ldouble2 *)(t.ab0 + (r * TX + 4 * q) * 2);
+      ldouble2 *p = (ldouble2 *)(t.ab0 + G::ab(r, 4 * q));  // 4 q .. 4 q + 3 share one 8-x block
 #pragma unroll
       for (int j = 0; j < 4; ++j) p[j] = dpair{A[j], B[j]};
     } else {
@@ -709,7 +714,7 @@ __device__ __forceinline__ void ywall8(const StencilArgs &a, const Tile7 &t) {
       const int rs = y + 2 * P - k - t.y0;  // tile row of input s = y + p - k
       const dpair c = ((lcdouble2 *)t.yc)[rs * W + k];
       if constexpr (BK != 0) {
-        const dpair v = ((lcdouble2 *)t.ab0)[rs * TX + t.lane];
+        const dpair v = *(lcdouble2 *)(t.ab0 + G::ab(rs, t.lane));
         dD = fma(c.x, v.x, dD);
         dE = fma(c.x, v.y, fma(c.y, v.x, dE));
       } else {
@@ -802,14 +807,14 @@ __device__ __forceinline__ void ysweep8(const StencilArgs &a, const Tile7 &t, do
 #pragma unroll
   for (int j = 0; j < R; ++j) D[j] = E[j] = 0.0;
   if constexpr (BK != 0) {
-    lcdouble2 *vp = (lcdouble2 *)t.ab0 + row0 * TX + t.lane;
+    lcdouble2 *vp = (lcdouble2 *)(t.ab0 + G::ab(row0, t.lane));
     dpair v[NR];
 #pragma unroll
-    for (int s = 0; s < PF && s < NR; ++s) v[s] = vp[s * TX];
+    for (int s = 0; s < PF && s < NR; ++s) v[s] = vp[s * (G::ABRS / 2)];
 #pragma unroll
     for (int s = 0; s < NR; ++s) {
       GDM_FENCE();
-      if (s + PF < NR) v[s + PF] = vp[(s + PF) * TX];
+      if (s + PF < NR) v[s + PF] = vp[(s + PF) * (G::ABRS / 2)];
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         const int k = s - j;  // row form: M(y_j, y_j - p + k)
