@@ -126,7 +126,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     from gdm_amd import GdmOperator
-    from gdm_amd.distributed import HaloExchange
+    from gdm_amd.distributed import HaloExchange, apply_overlapped
 
     p, n = args.p, args.n
     nz_cells = n if (args.strong or world == 1) else (n + 1) * world - 1
@@ -155,12 +155,18 @@ def main():
 
     def step(ev=None):
         if halo is not None:
-            halo.exchange(src)
-        if ev is not None:
-            ev[0].record(stream)
-        op.apply(src, dst)
-        if ev is not None:
-            ev[1].record(stream)
+            # ghost-plane exchange overlapped with the planes that need no ghosts
+            if ev is not None:
+                ev[0].record(stream)
+            apply_overlapped(op, halo, src, dst)
+            if ev is not None:
+                ev[1].record(stream)
+        else:
+            if ev is not None:
+                ev[0].record(stream)
+            op.apply(src, dst)
+            if ev is not None:
+                ev[1].record(stream)
         if bc is not None:
             op.add_boundary_data(bc, dst)
 

@@ -490,7 +490,9 @@ void build_faces(gdm_op *op) {
   keep(op, op->face_tmp);
 }
 
-hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst) {
+// Output planes [zb, ze) of the owned range (3D: z planes; the full owned
+// range otherwise).  dst is the owned vector; only those planes are written.
+hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst, int zb = -1, int ze = -1) {
   const gdm_layout &L = op->layout;
   gdmk::StencilArgs a{};
   a.src = src;
@@ -506,7 +508,12 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst)
     a.in_z0 = 0; a.in_z1 = 1; a.in_y0 = ib; a.in_y1 = ie;
     a.out_z0 = 0; a.out_z1 = 1; a.out_y0 = L.owned_plane_begin; a.out_y1 = L.owned_plane_end;
   }
-  a.zchunk = std::max(1, std::min(op->zchunk, a.out_z1 - a.out_z0));
+  if (zb < 0) zb = a.out_z0;
+  if (ze < 0) ze = a.out_z1;
+  zb = std::max(zb, a.out_z0);
+  ze = std::min(ze, a.out_z1);
+  if (ze <= zb) return hipSuccess;
+  a.zchunk = std::max(1, std::min(op->zchunk, ze - zb));
   a.x_toep = op->x_toep;
   a.y_toep = op->y_toep;
   a.z_toep = op->z_toep;
@@ -544,12 +551,18 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst)
 #endif
   if (L.n_owned == 0) return hipSuccess;
   const int bk = as_mass ? 0 : (op->kind == GDM_OP_WAVE ? 2 : 1);
-  if (!v8) return gdmk_launch_stencil(op->p, bk, a, op->stream);
+  if (!v8) {
+    // v7 indexes dst relative to out_z0: shift both to the sub-range
+    a.dst = dst + (int64_t)(zb - a.out_z0) * L.plane_size;
+    a.out_z0 = zb;
+    a.out_z1 = ze;
+    return gdmk_launch_stencil(op->p, bk, a, op->stream);
+  }
   // v8: output planes whose z columns are all interior (z' in [3p+1, Nz-3p-2])
   // go to the compile-time-band kernel; the rest (next to the z walls) to the
   // table kernel, both ranges of it in one launch.
   const int p = op->p, zlo = 3 * p + 1, zhi = a.Nz - 3 * p - 1;
-  const int i0 = std::max(a.out_z0, zlo), i1 = std::min(a.out_z1, zhi);
+  const int i0 = std::max(zb, zlo), i1 = std::min(ze, zhi);
   const bool split = a.z_toep && i1 - i0 >= 2 * p + 1 && !std::getenv("GDM_NO_ZINT");
   const int ty = ty8, wgs = wgs8;
   const int64_t tiles = (int64_t)((a.Nx + 63) / 64) * ((a.out_y1 - a.out_y0 + ty - 1) / ty);
@@ -560,8 +573,8 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst)
     return (int)std::max<int64_t>(std::min(len, 8), (len + chunks - 1) / chunks);
   };
   if (!split) {
-    a.cz0[0] = a.out_z0; a.cz1[0] = a.out_z1; a.cz0[1] = a.cz1[1] = 0;
-    a.zchunk = zchunk_for(a.out_z1 - a.out_z0);
+    a.cz0[0] = zb; a.cz1[0] = ze; a.cz0[1] = a.cz1[1] = 0;
+    a.zchunk = zchunk_for(ze - zb);
     a.nchunk0 = (a.cz1[0] - a.cz0[0] + a.zchunk - 1) / a.zchunk;
     return gdmk_launch_stencil8(p, bk, false, a, op->stream);
   }
@@ -572,11 +585,11 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst)
   hipError_t e = gdmk_launch_stencil8(p, bk, true, b, op->stream);
   if (e != hipSuccess) return e;
   // wall ranges [out_z0, i0) and [i1, out_z1)
-  a.cz0[0] = a.out_z0; a.cz1[0] = i0;
-  a.cz0[1] = i1; a.cz1[1] = a.out_z1;
-  a.zchunk = std::max(1, std::max(i0 - a.out_z0, a.out_z1 - i1));
-  a.nchunk0 = i0 > a.out_z0 ? 1 : 0;
-  if (i0 <= a.out_z0 && i1 >= a.out_z1) return hipSuccess;
+  a.cz0[0] = zb; a.cz1[0] = i0;
+  a.cz0[1] = i1; a.cz1[1] = ze;
+  a.zchunk = std::max(1, std::max(i0 - zb, ze - i1));
+  a.nchunk0 = i0 > zb ? 1 : 0;
+  if (i0 <= zb && i1 >= ze) return hipSuccess;
   return gdmk_launch_stencil8(p, bk, false, a, op->stream);
 }
 
@@ -751,6 +764,19 @@ int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const doub
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned), "stencil launch");
   if (bc_values) launch_boundary_data(op, bc_values, dst_owned);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_apply_planes(gdm_op *op, const double *src_local, double *dst_owned, int plane_begin, int plane_end) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
+  if (op->part_axis != 2 && (plane_begin > op->layout.owned_plane_begin || plane_end < op->layout.owned_plane_end))
+    return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_planes: plane sub-ranges need a 3D mesh");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, plane_begin, plane_end),
+            "stencil launch");
   return GDM_OK;
   GDM_GUARD_END
 }

@@ -79,6 +79,7 @@ def load():
         "gdm_op_use_own_stream": [P],
         "gdm_apply": [P, P, P, P],
         "gdm_add_boundary_data": [P, P, P],
+        "gdm_apply_planes": [P, P, P, i32, i32],
         "gdm_mass_apply": [P, P, P],
         "gdm_mass_solve": [P, P, P],
         "gdm_mass_solve_lines": [P, i32, P, i64, i64, i64, i64, i64],

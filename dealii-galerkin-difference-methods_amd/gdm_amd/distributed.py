@@ -205,3 +205,31 @@ class DistributedMassSolve:
             if npl[me] and b > a:
                 x2[:, a:b] = got[s]
         return x
+
+
+def apply_overlapped(op, halo, src_local, dst_owned, bc_values=None):
+    """compute_rhs of one slab with the ghost-plane exchange overlapped: the
+    output planes whose 2p+1 input planes are all owned are computed while the
+    exchange (update_ghost_values, advection/stiffness.h:343) is in flight, the
+    p planes next to each slab edge after it (gdm_apply_planes), then the inflow
+    boundary data.  `halo` may be None (single rank)."""
+    L = op.layout
+    p = L["halo_depth"]
+    pb, pe = L["owned_plane_begin"], L["owned_plane_end"]
+    lo = pb + (p if L["ghost_planes_below"] else 0)
+    hi = pe - (p if L["ghost_planes_above"] else 0)
+    reqs = halo.start(src_local) if halo is not None else []
+    if hi > lo:
+        op.apply_planes(src_local, dst_owned, lo, hi)
+    if halo is not None:
+        halo.finish(reqs)
+    if hi <= lo:
+        op.apply_planes(src_local, dst_owned, pb, pe)
+    else:
+        if lo > pb:
+            op.apply_planes(src_local, dst_owned, pb, lo)
+        if pe > hi:
+            op.apply_planes(src_local, dst_owned, hi, pe)
+    if bc_values is not None:
+        op.add_boundary_data(bc_values, dst_owned)
+    return dst_owned

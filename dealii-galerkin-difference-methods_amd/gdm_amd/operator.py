@@ -123,6 +123,13 @@ class GdmOperator:
         check(self.lib.gdm_apply(self.h, _ptr(src_local), _ptr(dst_owned), _ptr(bc_values)), "gdm_apply")
         return dst_owned
 
+    def apply_planes(self, src_local, dst_owned, plane_begin, plane_end):
+        """Volume term for the owned output planes [plane_begin, plane_end) only."""
+        self._check_sizes(src_local, dst_owned)
+        check(self.lib.gdm_apply_planes(self.h, _ptr(src_local), _ptr(dst_owned), int(plane_begin), int(plane_end)),
+              "gdm_apply_planes")
+        return dst_owned
+
     def add_boundary_data(self, bc_values, dst_owned):
         self._check_sizes(None, dst_owned)
         check(self.lib.gdm_add_boundary_data(self.h, _ptr(bc_values), _ptr(dst_owned)), "gdm_add_boundary_data")

@@ -136,6 +136,13 @@ int gdm_op_use_own_stream(gdm_op *op);
  * advection only: bc_values are the stage boundary values, device order, size
  * n_bc_points).  src_local has the full local layout (ghost planes filled). */
 int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const double *bc_values);
+/* The volume part of gdm_apply for the owned output planes [plane_begin,
+ * plane_end) of the last coordinate only (global plane indices; 3D).  Lets a
+ * multi-rank caller compute the planes that need no ghost data while the
+ * ghost-plane exchange is in flight, then the p planes next to each slab edge
+ * (the overlap of update_ghost_values, advection/stiffness.h:343, with the cell
+ * loop).  Boundary data: gdm_add_boundary_data afterwards. */
+int gdm_apply_planes(gdm_op *op, const double *src_local, double *dst_owned, int plane_begin, int plane_end);
 /* dst_owned += inflow boundary-data term only (the bc part of gdm_apply,
  * advection/stiffness.h:520-529 with a.n < 0); no-op for other kinds */
 int gdm_add_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned);

@@ -303,3 +303,23 @@ def test_mass_solve_lines_compose_to_mass_solve(dim, p, n):
     assert rel(host(x2), host(x1)) < 1e-14
     ref = m.kron_mass_inverse(host(r))
     assert rel(host(x2), ref) < 1e-12
+
+
+@pytest.mark.parametrize("n_ranks,rank", [(3, 1), (3, 0), (4, 3)])
+def test_apply_planes_overlap_split(n_ranks, rank):
+    """apply_overlapped's plane split (interior planes during the exchange,
+    the p planes at each slab edge after it) == one gdm_apply on that rank."""
+    g = _gdm()
+    from gdm_amd.distributed import apply_overlapped
+
+    shape, p = (100, 70, 120), 5
+    a = (0.7, -0.4, 0.3)
+    op = g.GdmOperator(3, p, shape, 0.0, 1.0, "advection", params=a, rank=rank, n_ranks=n_ranks)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    src = torch.rand(op.n_local, dtype=torch.float64, device="cuda", generator=gen)
+    bc = torch.rand(op.n_bc_points, dtype=torch.float64, device="cuda", generator=gen)
+    y1, y2 = op.new_vector(local=False), op.new_vector(local=False)
+    op.apply(src, y1, bc)
+    y2.fill_(7.0)
+    apply_overlapped(op, None, src, y2, bc)
+    assert rel(host(y2), host(y1)) < 1e-14
