@@ -580,8 +580,9 @@ __device__ __forceinline__ void wait_dma_planes(int wv) {
 // x-sweep of row group g (pass of this producer wave) into registers:
 // A = mhat*u (+ wall rows), B = sx bhat*u (+ wall rows), 4 consecutive x per lane
 template <int P, int R, int NC, int NP, int BK>
-__device__ __forceinline__ void xsweep8(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g, double (&A)[4],
-                                        double (&B)[4]) {
+__device__ __forceinline__ void xsweep8(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g, dpair (&V)[4]) {
+  // V[j] = (A_j, B_j) for x = 4 q + j (the pair the AB plane stores, so no
+  // register moves before the b128 stores); mass: V[0] = (A_0, A_1), V[1] = (A_2, A_3)
   using G = Geom8<P, R, NC, NP, BK>;
   using IR = InteriorRows<P>;
   constexpr int W = G::W, RL = G::RL;
@@ -596,19 +597,28 @@ __device__ __forceinline__ void xsweep8(const StencilArgs &a, const Tile7 &t, lc
     w[2 * i + 1] = v.y;
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) A[j] = B[j] = 0.0;
+  for (int j = 0; j < 4; ++j) V[j] = dpair{0.0, 0.0};
   if (a.x_toep) {
 #pragma unroll
     for (int k = 0; k < W; ++k)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        A[j] = fma(IR::m[k], w[j + k + 1], A[j]);
-        if constexpr (BK == 1) B[j] = fma(IR::c[k], w[j + k + 1], B[j]);
-        if constexpr (BK == 2) B[j] = fma(IR::l[k], w[j + k + 1], B[j]);
+        if constexpr (BK == 0) {
+          if (j % 2 == 0)
+            V[j / 2].x = fma(IR::m[k], w[j + k + 1], V[j / 2].x);
+          else
+            V[j / 2].y = fma(IR::m[k], w[j + k + 1], V[j / 2].y);
+        } else {
+          V[j].x = fma(IR::m[k], w[j + k + 1], V[j].x);
+          if constexpr (BK == 1) V[j].y = fma(IR::c[k], w[j + k + 1], V[j].y);
+          if constexpr (BK == 2) V[j].y = fma(IR::l[k], w[j + k + 1], V[j].y);
+        }
       }
   }
+  if constexpr (BK != 0) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) B[j] *= a.sx;
+    for (int j = 0; j < 4; ++j) V[j].y *= a.sx;
+  }
 }
 
 // Wall columns of row group g (first / last x tiles only): the
@@ -663,7 +673,7 @@ __device__ __forceinline__ void xwall8_add(const Tile7 &t, const XWall<P, BK> &x
 
 // store row group g's (A, B) into the interleaved plane buffer
 template <int P, int R, int NC, int NP, int BK>
-__device__ __forceinline__ void write_ab8(const Tile7 &t, int g, const double (&A)[4], const double (&B)[4]) {
+__device__ __forceinline__ void write_ab8(const Tile7 &t, int g, const dpair (&V)[4]) {
   using G = Geom8<P, R, NC, NP, BK>;
   constexpr int TX = G::TX;
   const int rr = t.lane >> 4, q = t.lane & 15;
@@ -672,11 +682,11 @@ __device__ __forceinline__ void write_ab8(const Tile7 &t, int g, const double (&
     if constexpr (BK != 0) {
       ldouble2 *p = (ldouble2 *)(t.ab0 + G::ab(r, 4 * q));  // 4 q .. 4 q + 3 share one 8-x block
 #pragma unroll
-      for (int j = 0; j < 4; ++j) p[j] = dpair{A[j], B[j]};
+      for (int j = 0; j < 4; ++j) p[j] = V[j];
     } else {
       ldouble2 *p = (ldouble2 *)(t.ab0 + r * TX + 4 * q);
-      p[0] = dpair{A[0], A[1]};
-      p[1] = dpair{A[2], A[3]};
+      p[0] = V[0];
+      p[1] = V[1];
     }
   }
 }
@@ -738,7 +748,7 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
   for (int k = 0; k < NS; ++k)
     if (k < n) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + k, u[k]);
   GDM_LDS_BARRIER();  // tables in LDS
-  double AR[4], BR[4];
+  dpair V1[4];
   int slot = 0;
   for (int i = 0; i < n; ++i) {
     const int rem = n - 1 - i;  // planes issued after plane i (at most NS - 1)
@@ -752,10 +762,10 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
       GDM_WAIT_VMCNT(0);
     // the first two row groups into registers before F (overlapping the
     // consumers' y-sweep of plane i - 1), any further ones straight into AB
-    double AR2[4], BR2[4];
-    if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], t.wv, AR, BR);
+    dpair V2[4];
+    if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], t.wv, V1);
     const bool two = G::NPASS > 1 && t.wv + NP < G::NG;
-    if (two && !GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], t.wv + NP, AR2, BR2);
+    if (two && !GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], t.wv + NP, V2);
     XWall<P, BK> xw0, xw1;
     if (t.ncw > 0) {
       xwall8_calc<P, R, NC, NP, BK>(a, t, u[slot], t.wv, xw0);
@@ -766,8 +776,8 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
       GDM_LDS_BARRIER();               // M_i-1
     }
     GDM_LDS_BARRIER();  // F_i
-    write_ab8<P, R, NC, NP, BK>(t, t.wv, AR, BR);
-    if (two) write_ab8<P, R, NC, NP, BK>(t, t.wv + NP, AR2, BR2);
+    write_ab8<P, R, NC, NP, BK>(t, t.wv, V1);
+    if (two) write_ab8<P, R, NC, NP, BK>(t, t.wv + NP, V2);
     if (t.ncw > 0) {
       xwall8_add<P, BK>(t, xw0);
       if (two) xwall8_add<P, BK>(t, xw1);
@@ -776,8 +786,8 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
     for (int ps = 2; ps < G::NPASS; ++ps) {
       const int g = t.wv + ps * NP;
       if (g < G::NG) {
-        if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], g, AR, BR);
-        write_ab8<P, R, NC, NP, BK>(t, g, AR, BR);
+        if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], g, V1);
+        write_ab8<P, R, NC, NP, BK>(t, g, V1);
         if (t.ncw > 0) {
           xwall8_calc<P, R, NC, NP, BK>(a, t, u[slot], g, xw0);
           xwall8_add<P, BK>(t, xw0);
