@@ -59,6 +59,9 @@ struct FaceDir {
   int *qs = nullptr, *qc = nullptr;
   double *w = nullptr;    // [n_nodes][wmax]
   double *wT = nullptr;   // [wmax][n_nodes]
+  double *phi = nullptr;  // [p][p+1][p+1] cell tables (cell form of the face step 1)
+  int *crange = nullptr;  // [n_nodes][2] first / last local cell of each node
+  int ncell_total = 0;
 };
 
 struct Face {
@@ -456,6 +459,24 @@ void build_faces(gdm_op *op) {
       t.qs = keep(op, dev_upload(ft.qstart));
       t.qc = keep(op, dev_upload(ft.qcount));
       t.w = keep(op, dev_upload(ft.w));
+      {
+        // cell form: per-category tables and the cell range of every node
+        std::vector<double> xq, wq;
+        gdm::gauss_unit(n1, xq, wq);
+        std::vector<double> phi((size_t)p * n1 * n1);
+        for (int cat = 0; cat < p; ++cat)
+          for (int l = 0; l < n1; ++l)
+            for (int qq = 0; qq < n1; ++qq)
+              phi[((size_t)cat * n1 + l) * n1 + qq] = gdm::shape_1d(p, cat, l, xq[qq], 0) * wq[qq] * h;
+        std::vector<int32_t> cr((size_t)2 * ft.n_nodes);
+        for (int i = 0; i < ft.n_nodes; ++i) {
+          cr[2 * i] = ft.qstart[i] / n1;
+          cr[2 * i + 1] = ft.qstart[i] / n1 + ft.qcount[i] / n1 - 1;
+        }
+        t.phi = keep(op, dev_upload(phi));
+        t.crange = keep(op, dev_upload(cr));
+        t.ncell_total = (int)nce;
+      }
     }
     F.n_points = (int64_t)F.t0.Q * F.t1.Q;
     F.offset = offset;
@@ -615,6 +636,11 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
       fa.qc1 = F.t1.qc;
       fa.w1 = F.t1.w;
       fa.wmax1 = F.t1.wmax;
+      fa.phi0 = F.t0.phi;
+      fa.crange0 = F.t0.crange;
+      fa.p = op->p;
+      fa.ncell0_total = F.t0.ncell_total;
+      fa.cell0_begin = F.t0.cell_begin;
       fa.T = op->face_tmp;
       fa.dst = dst_owned;
       fa.base = F.base;

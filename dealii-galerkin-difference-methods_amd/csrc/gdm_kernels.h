@@ -60,6 +60,12 @@ struct FaceArgs {
   const double *w1;   // [n_nodes1][wmax1]: weights of t1, node-major (wave-uniform rows)
   int wmax0, wmax1, ldw0;
   int qmax0;  // largest q-range of FACE_CHUNK consecutive t0 nodes (LDS row length)
+  // cell form of step 1 (t0 non-trivial and its local cells fit LDS): Phi0 =
+  // [category][l][q] values phi_l(x_q) w_q h of t0, crange0[2 i] / [2 i + 1] =
+  // first / last local cell of node i
+  const double *phi0;
+  const int *crange0;
+  int p, ncell0_total, cell0_begin;
   double *T;  // scratch Q1 x (i0_end - i0_begin)
   double *dst;
   int64_t base, stride0, stride1;  // dst offset of node (i0_begin, i1_begin)
