@@ -75,6 +75,9 @@ struct Face {
 
 }  // namespace
 
+// shared with the sparse-matrix entry points (gdm_csr.hip)
+int gdm_internal_set_error(int code, const char *msg) { return fail(code, msg); }
+
 struct gdm_op {
   int device = 0;
   hipStream_t own_stream = nullptr, stream = nullptr;

@@ -7,5 +7,6 @@ operator classes.  No CPU fallback exists.
 """
 from ._capi import GdmError, load, declared_symbols, device_count  # noqa: F401
 from .operator import GdmOperator  # noqa: F401
+from .sparse import SparseMatrix, solve_cg  # noqa: F401
 
-__all__ = ["GdmError", "GdmOperator", "load", "declared_symbols", "device_count"]
+__all__ = ["GdmError", "GdmOperator", "SparseMatrix", "solve_cg", "load", "declared_symbols", "device_count"]

@@ -93,6 +93,16 @@ def load():
         "gdm_bc_points": [P, P],
         "gdm_bc_reference_order": [P, P],
         "gdm_time_op": [P, i32, P, P, P, i32, ctypes.POINTER(d)],
+        "gdm_csr_create": [i32, i64, i64, i64, P, P, P, i32, ctypes.POINTER(P)],
+        "gdm_csr_destroy": [P],
+        "gdm_csr_info": [P, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64)],
+        "gdm_csr_set_stream": [P, P],
+        "gdm_csr_download": [P, P, P, P],
+        "gdm_csr_vmult": [P, P, P],
+        "gdm_csr_cg": [P, P, P, i32, i32, d, d, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(d)],
+        "gdm_csr_read_triplets": [i32, ctypes.c_char_p, i32, ctypes.POINTER(P)],
+        "gdm_csr_write_triplets": [P, ctypes.c_char_p, i32],
+        "gdm_csr_time_vmult": [P, P, P, i32, ctypes.POINTER(d)],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

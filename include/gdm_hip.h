@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 2
+#define GDM_HIP_ABI_VERSION 3
 
 enum gdm_status {
   GDM_OK = 0,
@@ -185,6 +185,53 @@ int gdm_bc_reference_order(const gdm_op *op, int64_t *ref_to_dev_host);
  * avg_ms_host receives the mean time per application. */
 int gdm_time_op(gdm_op *op, int which, const double *src, double *dst, const double *bc_values, int n_iter,
                 double *avg_ms_host);
+
+/* ------------------------------------------------------------------------
+ * Assembled sparse matrices: the irregular-stencil CG of
+ * the cut-cell Poisson prototype and the on-disk triplet format.
+ *
+ *   gdm_csr_create       dealii::SparseMatrix<double>::reinit(sparsity) + the
+ *                        assembled values (prototypes/cut_poisson_01_gdm.cc:
+ *                        148-163, 327-336; full structural stencil of
+ *                        System::create_sparsity_pattern, system.h:586-599).
+ *                        Arrays are copied into device memory owned by the
+ *                        handle; row_ptr int64 (n_rows+1), cols uint32 (the
+ *                        reference's unsigned int indices), vals fp64.
+ *                        src_is_device: 1 = the three arrays are device
+ *                        pointers, 0 = host pointers.
+ *   gdm_csr_vmult        SparseMatrix::vmult(dst, src) -- the matvec SolverCG
+ *                        calls (cut_poisson_01_gdm.cc:335)
+ *   gdm_csr_cg           SolverCG<>(ReductionControl(max_it, abs_tol, rel_tol))
+ *                        .solve(A, x, b, P) with P = PreconditionIdentity
+ *                        (precond 0, cut_poisson_01_gdm.cc:332-335) or
+ *                        PreconditionJacobi (precond 1, omega = 1); x is the
+ *                        initial guess; *its_host = last_step, *res_host = final
+ *                        residual norm; GDM_ERR_STATE when max_it is reached.
+ *   gdm_csr_read_triplets / gdm_csr_write_triplets
+ *                        the binary / text triplet files of write_matrix_to_file
+ *                        (applications/wave/wave-ev.cc:93-127): per entry u32
+ *                        row, u32 column, f64 value (binary) or "row col value"
+ *                        lines (text), rows ascending, diagonal first in each
+ *                        square-matrix row (deal.II SparsityPattern order).
+ *                        Reading sums duplicate (row, col) entries.
+ * ---------------------------------------------------------------------- */
+typedef struct gdm_csr gdm_csr;
+
+int gdm_csr_create(int device, int64_t n_rows, int64_t n_cols, int64_t nnz, const int64_t *row_ptr,
+                   const uint32_t *cols, const double *vals, int src_is_device, gdm_csr **out);
+int gdm_csr_destroy(gdm_csr *A);
+int gdm_csr_info(const gdm_csr *A, int64_t *n_rows, int64_t *n_cols, int64_t *nnz);
+int gdm_csr_set_stream(gdm_csr *A, void *hip_stream);
+/* host copies of the three arrays (caller-allocated, sizes from gdm_csr_info) */
+int gdm_csr_download(const gdm_csr *A, int64_t *row_ptr_host, uint32_t *cols_host, double *vals_host);
+/* dst = A src (device pointers, dst of n_rows, src of n_cols entries) */
+int gdm_csr_vmult(gdm_csr *A, const double *src, double *dst);
+int gdm_csr_cg(gdm_csr *A, const double *b, double *x, int precond, int max_it, double abs_tol, double rel_tol,
+               int *its_host, double *res_host);
+int gdm_csr_read_triplets(int device, const char *path, int binary, gdm_csr **out);
+int gdm_csr_write_triplets(const gdm_csr *A, const char *path, int binary);
+/* mean time of n_iter back-to-back gdm_csr_vmult calls (HIP events, ms) */
+int gdm_csr_time_vmult(gdm_csr *A, const double *src, double *dst, int n_iter, double *avg_ms_host);
 
 #ifdef __cplusplus
 }
