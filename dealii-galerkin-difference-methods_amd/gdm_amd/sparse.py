@@ -61,6 +61,8 @@ class SparseMatrix:
         check(self._lib.gdm_csr_create(device, n_rows, int(n_cols), nnz, ptrs[0], ptrs[1], ptrs[2],
                                        1 if on_device else 0, ctypes.byref(self._h)), "gdm_csr_create")
         del keep
+        # order every launch after torch's own work on its tensors (fills, copies)
+        self.use_torch_stream()
 
     @classmethod
     def from_scipy(cls, A, device=0):
@@ -74,7 +76,9 @@ class SparseMatrix:
         h = ctypes.c_void_p()
         check(_capi.load().gdm_csr_read_triplets(device, str(path).encode(), 1 if binary else 0, ctypes.byref(h)),
               "gdm_csr_read_triplets")
-        return cls(None, None, None, device=device, _handle=h)
+        A = cls(None, None, None, device=device, _handle=h)
+        A.use_torch_stream()
+        return A
 
     def write_triplets(self, path, binary=True):
         check(self._lib.gdm_csr_write_triplets(self._h, str(path).encode(), 1 if binary else 0),

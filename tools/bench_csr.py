@@ -44,8 +44,16 @@ def main():
     torch.cuda.synchronize()
     import time
 
+    # a fixed number of CG iterations (the synthetic matrix is not the cut
+    # Poisson system, so its iteration count means nothing; the cost per
+    # iteration does)
+    cg_its = 100
     t0 = time.perf_counter()
-    its, res = sp.solve_cg(A, xs, b, "identity", max_it=rows, abs_tol=1e-10, rel_tol=1e-6)
+    try:
+        its, res = sp.solve_cg(A, xs, b, "identity", max_it=cg_its, abs_tol=1e-300, rel_tol=1e-300)
+    except sp.GdmError:
+        its, res = cg_its, None
+    torch.cuda.synchronize()
     cg_s = time.perf_counter() - t0
     out = {
         "metric": "CSR vmult (cut-Poisson CG matvec, config 5)",
@@ -54,7 +62,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": alg / (ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
                      "frac": alg / (ms * 1e-3) / 1e9 / 8000.0, "algorithmic_bytes_per_launch": alg},
         "cg": {"iterations": its, "residual": res, "seconds": cg_s, "ms_per_iteration": cg_s * 1e3 / max(its, 1),
-               "tolerances": "ReductionControl(rows, 1e-10, 1e-6), PreconditionIdentity"},
+               "setup": "100 iterations of SolverCG + PreconditionIdentity (cut_poisson_01_gdm.cc:332-335)"},
         "data": "synthetic SPD Kronecker-sum values on the full structural stencil",
     }
     print(json.dumps(out), flush=True)
