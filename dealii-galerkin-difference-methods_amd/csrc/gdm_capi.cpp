@@ -101,6 +101,8 @@ struct gdm_op {
   double sx8 = 0, cy8[19] = {0};
   double dint = 0, m_dint = 0;  // interior z scales of D (operator, mass)
   int stencil_version = 8;
+  int mass_version = 2;   // GDM_MASS=1: v1 in-place one-thread-per-line sweeps
+  int mass_max_wgs = 0;   // GDM_MASS_WGS: cap on the line-solve grid (0 = all lines)
   // the same for the mass operator of an advection/wave op (gdm_mass_apply)
   double *m_corrX = nullptr, *m_zt = nullptr;
   double *lrow[3] = {nullptr, nullptr, nullptr}, *invd[3] = {nullptr, nullptr, nullptr};
@@ -743,6 +745,8 @@ int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int
   build_faces(op);
   op->zchunk = choose_zchunk(op);
   if (const char *env = std::getenv("GDM_STENCIL")) op->stencil_version = std::atoi(env) == 7 ? 7 : 8;
+  if (const char *env = std::getenv("GDM_MASS")) op->mass_version = std::atoi(env) == 1 ? 1 : 2;
+  if (const char *env = std::getenv("GDM_MASS_WGS")) op->mass_max_wgs = std::max(0, std::atoi(env));
   hip_check(hipMalloc(&op->dot_partial, sizeof(double) * op->n_dot_partial), "hipMalloc");
   keep(op, op->dot_partial);
   hip_check(hipMalloc(&op->dot_out, sizeof(double)), "hipMalloc");
@@ -838,21 +842,42 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   const int64_t n = op->layout.n_owned;
-  if (x_owned != rhs_owned)
-    hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
   const int64_t X = op->K[0], Y = op->K[1], Z = op->K[2];
-  // z lines: (x, y) -> base = l, stride X*Y
-  if (Z > 1)
-    hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)Z, X * Y, X * Y, X * Y, 0, 1, op->lrow[2], op->invd[2],
-                                     op->stream), "chol z");
-  // y lines: (x, z) -> base = z*X*Y + x, stride X
-  if (Y > 1)
-    hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)Y, X, X * Z, X, X * Y, 1, op->lrow[1], op->invd[1],
-                                     op->stream), "chol y");
-  // x lines: (y, z) -> base = l*X, stride 1
-  if (X > 1)
-    hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)X, 1, Y * Z, Y * Z, 0, X, op->lrow[0], op->invd[0],
-                                     op->stream), "chol x");
+  if (op->mass_version == 1) {
+    // v1: in-place sweeps, one thread per line (kept for A/B timing)
+    if (x_owned != rhs_owned)
+      hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+    if (Z > 1)
+      hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)Z, X * Y, X * Y, X * Y, 0, 1, op->lrow[2], op->invd[2],
+                                       op->stream), "chol z");
+    if (Y > 1)
+      hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)Y, X, X * Z, X, X * Y, 1, op->lrow[1], op->invd[1],
+                                       op->stream), "chol y");
+    if (X > 1)
+      hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)X, 1, Y * Z, Y * Z, 0, X, op->lrow[0], op->invd[0],
+                                       op->stream), "chol x");
+    return GDM_OK;
+  }
+  // v2 (gdm_mass.hip): the first pass reads rhs and writes x, later passes in place
+  const double *in = rhs_owned;
+  const int wg = op->mass_max_wgs;
+  if (Z > 1) {  // z lines: (x, y) -> base = l, step X*Y
+    hip_check(gdmk_launch_mass_lines(op->p, 1, in, x_owned, (int)Z, X * Y, X * Y, X * Y, 0, op->lrow[2], op->invd[2],
+                                     wg, op->stream), "mass z");
+    in = x_owned;
+  }
+  if (Y > 1) {  // y lines: (x, z) -> base = z*X*Y + x, step X
+    hip_check(gdmk_launch_mass_lines(op->p, 1, in, x_owned, (int)Y, X, X * Z, X, X * Y, op->lrow[1], op->invd[1], wg,
+                                     op->stream), "mass y");
+    in = x_owned;
+  }
+  if (X > 1) {  // x lines: contiguous rows of length X
+    hip_check(gdmk_launch_mass_lines(op->p, 0, in, x_owned, (int)X, 1, Y * Z, 1, 0, op->lrow[0], op->invd[0], wg,
+                                     op->stream), "mass x");
+    in = x_owned;
+  }
+  if (in != x_owned)
+    hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
   return GDM_OK;
   GDM_GUARD_END
 }

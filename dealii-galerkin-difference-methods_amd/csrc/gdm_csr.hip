@@ -39,7 +39,11 @@ namespace {
 constexpr int CSR_BLOCK = 256;
 constexpr int RED_BLOCK = 1024;
 // device scalar slots of the CG
-enum { S_RR = 0, S_GH = 1, S_GH_OLD = 2, S_PAP = 3, S_ALPHA = 4, S_BETA = 5, S_N = 8 };
+// r.z of iteration k (k = 0: initial residual) lives in S_GH + (k & 1).  No
+// kernel reads a slot it writes: a uniform read may be served by the scalar
+// cache and then observe the same wave's later vector store to that address
+// (the round-1 CG defect, gh_old == gh after an iteration).
+enum { S_RR = 0, S_GH = 1, S_PAP = 3, S_N = 8 };
 
 int fail(int code, const std::string &msg) { return gdm_internal_set_error(code, msg.c_str()); }
 
@@ -107,15 +111,13 @@ __global__ void __launch_bounds__(CSR_BLOCK) csr_spmv_kernel(int64_t n_rows, con
 }
 
 // deterministic sum of nparts partials (stride 1) of `nval` arrays laid out
-// back to back (part[j * nparts + i]) and the CG scalar update of `mode`
-//   mode 0: S[RR] = s0, S[GH] = s1                      (initial residual)
-//   mode 1: S[PAP] = s0, S[ALPHA] = S[GH] / S[PAP]
-//   mode 2: S[RR] = s0, S[GH_OLD] = S[GH], S[GH] = s1, S[BETA] = S[GH] / S[GH_OLD]
-//   mode 3: S[0] = s0                                   (plain dot)
+// back to back (part[j * nparts + i]); results are written, never read:
+//   S[slot0] = sum 0, S[slot1] = sum 1 (nval == 2)
 __global__ void __launch_bounds__(RED_BLOCK) cg_reduce_kernel(const double *__restrict__ part, int64_t nparts,
-                                                              int nval, int mode, double *__restrict__ S) {
+                                                              int nval, int slot0, int slot1,
+                                                              double *__restrict__ S) {
   __shared__ double sh[RED_BLOCK / 64];
-  double r[2];
+  double r[2] = {0.0, 0.0};
   for (int j = 0; j < nval; ++j) {
     double a = 0.0;
     for (int64_t i = threadIdx.x; i < nparts; i += RED_BLOCK) a += part[j * nparts + i];
@@ -128,20 +130,8 @@ __global__ void __launch_bounds__(RED_BLOCK) cg_reduce_kernel(const double *__re
     __syncthreads();
   }
   if (threadIdx.x != 0) return;
-  if (mode == 0) {
-    S[S_RR] = r[0];
-    S[S_GH] = r[1];
-  } else if (mode == 1) {
-    S[S_PAP] = r[0];
-    S[S_ALPHA] = S[S_GH] / r[0];
-  } else if (mode == 2) {
-    S[S_RR] = r[0];
-    S[S_GH_OLD] = S[S_GH];
-    S[S_GH] = r[1];
-    S[S_BETA] = r[1] / S[S_GH_OLD];
-  } else {
-    S[0] = r[0];
-  }
+  S[slot0] = r[0];
+  if (nval > 1) S[slot1] = r[1];
 }
 
 // partials of r.r and r.(dinv r) (dinv NULL = identity)
@@ -165,28 +155,30 @@ __global__ void __launch_bounds__(CSR_BLOCK) cg_init_kernel(int64_t n, const dou
   }
 }
 
-// p = z + beta p  (first: p = z), z = dinv r
+// iteration it: p = z + beta p (it == 1: p = z), z = dinv r,
+// beta = gh(it - 1) / gh(it - 2)
 __global__ void __launch_bounds__(CSR_BLOCK) cg_dir_kernel(int64_t n, const double *__restrict__ r,
                                                            const double *__restrict__ dinv, double *__restrict__ p,
-                                                           const double *__restrict__ S, int first) {
+                                                           const double *__restrict__ S, int it) {
   const int64_t i = (int64_t)blockIdx.x * CSR_BLOCK + threadIdx.x;
   if (i >= n) return;
   const double z = dinv ? dinv[i] * r[i] : r[i];
-  p[i] = first ? z : z + S[S_BETA] * p[i];
+  p[i] = it == 1 ? z : z + (S[S_GH + ((it - 1) & 1)] / S[S_GH + (it & 1)]) * p[i];
 }
 
-// x += alpha p ; r -= alpha q ; partials of r.r and r.z
+// iteration it: x += alpha p ; r -= alpha q with alpha = gh(it - 1) / p.Ap ;
+// partials of r.r and r.z
 __global__ void __launch_bounds__(CSR_BLOCK) cg_update_kernel(int64_t n, double *__restrict__ x,
                                                               double *__restrict__ r, const double *__restrict__ p,
                                                               const double *__restrict__ q,
                                                               const double *__restrict__ dinv,
-                                                              const double *__restrict__ S,
+                                                              const double *__restrict__ S, int it,
                                                               double *__restrict__ part, int64_t nparts) {
   __shared__ double sh[CSR_BLOCK / 64];
   const int64_t i = (int64_t)blockIdx.x * CSR_BLOCK + threadIdx.x;
   double rr = 0.0, rz = 0.0;
   if (i < n) {
-    const double alpha = S[S_ALPHA];
+    const double alpha = S[S_GH + ((it - 1) & 1)] / S[S_PAP];
     x[i] += alpha * p[i];
     const double ri = r[i] - alpha * q[i];
     r[i] = ri;
@@ -368,6 +360,9 @@ int create_impl(int device, int64_t n_rows, int64_t n_cols, int64_t nnz, const i
     hip_check(hipMalloc(&A->v, sizeof(double) * std::max<int64_t>(nnz, 1)), "hipMalloc vals");
     const hipMemcpyKind kind = src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     if (!src_is_device) validate_host(n_rows, n_cols, nnz, rp, ci);
+    // device sources may still be written by work queued on other streams (the
+    // caller's fills and conversions): this setup call orders after all of it
+    if (src_is_device) hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     hip_check(hipMemcpyAsync(A->rp, rp, sizeof(int64_t) * (n_rows + 1), kind, A->stream), "copy row_ptr");
     if (nnz > 0) {
       hip_check(hipMemcpyAsync(A->ci, ci, sizeof(uint32_t) * nnz, kind, A->stream), "copy cols");
@@ -428,6 +423,50 @@ double read_scalar(gdm_csr *A, int slot) {
   hip_check(hipStreamSynchronize(A->stream), "sync");
   return A->S_host[0];
 }
+
+// GDM_CG_TRACE=1: after every CG iteration download the device state and check
+// the recurrence invariants on the host (debugging aid; prints to stderr)
+struct CgTrace {
+  bool on = false;
+  std::vector<int64_t> rp;
+  std::vector<uint32_t> ci;
+  std::vector<double> v, r, p, q, x, S;
+  void init(gdm_csr *A) {
+    on = std::getenv("GDM_CG_TRACE") != nullptr;
+    if (!on) return;
+    rp.resize(A->n_rows + 1);
+    ci.resize(std::max<int64_t>(A->nnz, 1));
+    v.resize(std::max<int64_t>(A->nnz, 1));
+    hip_check(hipStreamSynchronize(A->stream), "sync");
+    hip_check(hipMemcpy(rp.data(), A->rp, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost), "d2h");
+    hip_check(hipMemcpy(ci.data(), A->ci, sizeof(uint32_t) * ci.size(), hipMemcpyDeviceToHost), "d2h");
+    hip_check(hipMemcpy(v.data(), A->v, sizeof(double) * v.size(), hipMemcpyDeviceToHost), "d2h");
+  }
+  void step(gdm_csr *A, const double *xd, int it) {
+    if (!on) return;
+    const int64_t n = A->n_rows;
+    r.resize(n); p.resize(n); q.resize(n); x.resize(n); S.resize(S_N);
+    hip_check(hipStreamSynchronize(A->stream), "sync");
+    hip_check(hipMemcpy(r.data(), A->r, sizeof(double) * n, hipMemcpyDeviceToHost), "d2h");
+    hip_check(hipMemcpy(p.data(), A->p, sizeof(double) * n, hipMemcpyDeviceToHost), "d2h");
+    hip_check(hipMemcpy(q.data(), A->q, sizeof(double) * n, hipMemcpyDeviceToHost), "d2h");
+    hip_check(hipMemcpy(x.data(), xd, sizeof(double) * n, hipMemcpyDeviceToHost), "d2h");
+    hip_check(hipMemcpy(S.data(), A->S, sizeof(double) * S_N, hipMemcpyDeviceToHost), "d2h");
+    double rr = 0, pap = 0, dq = 0, nq = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      double s = 0;
+      for (int64_t k = rp[i]; k < rp[i + 1]; ++k) s += v[k] * p[ci[k]];
+      dq = std::max(dq, std::fabs(s - q[i]));
+      nq = std::max(nq, std::fabs(s));
+      rr += r[i] * r[i];
+      pap += p[i] * s;
+    }
+    std::fprintf(stderr,
+                 "[cg-trace] it %d  S: rr %.6e gh %.6e gh_old %.6e pap %.6e | host rr %.6e pap %.6e |Ap-q| %.3e "
+                 "of %.3e\n",
+                 it, S[S_RR], S[S_GH + (it & 1)], S[S_GH + ((it - 1) & 1)], S[S_PAP], rr, pap, dq, nq);
+  }
+};
 
 }  // namespace
 
@@ -509,19 +548,22 @@ int gdm_csr_cg(gdm_csr *A, const double *b, double *x, int precond, int max_it, 
     // r = b - A x ; r.r ; r.z
     hip_check(launch_spmv(A, x, b, A->r, nullptr), "spmv launch");
     cg_init_kernel<<<gv, CSR_BLOCK, 0, A->stream>>>(n, A->r, dinv, A->part, gv);
-    cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, gv, 2, 0, A->S);
+    cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, gv, 2, S_RR, S_GH, A->S);
     hip_check(hipGetLastError(), "cg init");
     res = std::sqrt(read_scalar(A, S_RR));
     const double tol = std::max(abs_tol, rel_tol * res);
     bool converged = res <= tol;
+    CgTrace trace;
+    trace.init(A);
     while (!converged && its < max_it) {
       ++its;
-      cg_dir_kernel<<<gv, CSR_BLOCK, 0, A->stream>>>(n, A->r, dinv, A->p, A->S, its == 1);
+      cg_dir_kernel<<<gv, CSR_BLOCK, 0, A->stream>>>(n, A->r, dinv, A->p, A->S, its);
       hip_check(launch_spmv(A, A->p, nullptr, A->q, A->part), "spmv launch");
-      cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, ns, 1, 1, A->S);
-      cg_update_kernel<<<gv, CSR_BLOCK, 0, A->stream>>>(n, x, A->r, A->p, A->q, dinv, A->S, A->part, gv);
-      cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, gv, 2, 2, A->S);
+      cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, ns, 1, S_PAP, S_PAP, A->S);
+      cg_update_kernel<<<gv, CSR_BLOCK, 0, A->stream>>>(n, x, A->r, A->p, A->q, dinv, A->S, its, A->part, gv);
+      cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, gv, 2, S_RR, S_GH + (its & 1), A->S);
       hip_check(hipGetLastError(), "cg iteration");
+      if (its <= 40) trace.step(A, x, its);
       res = std::sqrt(read_scalar(A, S_RR));
       converged = res <= tol;
     }

@@ -84,6 +84,11 @@ int gdmk_stencil_tile_rows(int p);
 void gdmk_stencil8_geom(int p, int *tile_rows, int *wgs_per_cu);
 hipError_t gdmk_launch_chol_lines(int p, double *v, int len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,
                                   int64_t C, const double *lrow, const double *inv_diag, hipStream_t st);
+// mass inverse v2 line solves (gdm_mass.hip): dir_kind 0 = contiguous lines
+// (line l at l * len), 1 = strided lines (base (l / A) * B + l % A, step stride)
+hipError_t gdmk_launch_mass_lines(int p, int dir_kind, const double *src, double *dst, int len, int64_t stride,
+                                  int64_t n_lines, int64_t A, int64_t B, const double *lrow, const double *inv_diag,
+                                  int max_wgs, hipStream_t st);
 hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st);
 hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st);
 hipError_t gdmk_launch_dot(int64_t n, const double *x, const double *y, double *partial, int n_partial, double *out,

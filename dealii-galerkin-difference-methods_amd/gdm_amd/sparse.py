@@ -123,7 +123,7 @@ class SparseMatrix:
     def use_torch_stream(self):
         import torch
 
-        check(self._lib.gdm_csr_set_stream(self._h, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+        check(self._lib.gdm_csr_set_stream(self._h, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
               "gdm_csr_set_stream")
 
     def vmult(self, dst, src):

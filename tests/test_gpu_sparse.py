@@ -132,9 +132,6 @@ def _sum_csr(a, b):
 
 @pytest.mark.parametrize("dim,p,n", [(1, 3, 64), (2, 3, 16), (2, 5, 12), (3, 3, 7)])
 @pytest.mark.parametrize("precond", ["identity", "jacobi"])
-@pytest.mark.xfail(reason="KNOWN DEFECT (r1s3c on MI355X): device CG needs 2-20x the oracle's iterations "
-                          "(e.g. 555 vs 25); SpMV itself is parity-green -- open bug in the fused CG update",
-                   strict=False)
 def test_cg_vs_oracle(dim, p, n, precond):
     """SPD systems: mass (advection/problem.h:236-267 tolerances) and
     Laplace + mass (cut_poisson_01_gdm.cc:330-335 tolerances)."""
@@ -148,14 +145,17 @@ def test_cg_vs_oracle(dim, p, n, precond):
         x_ref, its_ref = O.cg(rp, cols, vals, b, precond=pc, max_it=5000, abs_tol=abs_tol, rel_tol=rel_tol)
         assert its_ref > 0
         A = sp.SparseMatrix(rp, cols.astype(np.uint32), vals)
-        x = torch.zeros(m.n_dofs, dtype=torch.float64, device="cuda")
-        its, res = sp.solve_cg(A, x, dev(b), preconditioner=precond, max_it=5000, abs_tol=abs_tol,
-                               rel_tol=rel_tol)
-        assert abs(its - its_ref) <= 1, (its, its_ref)
-        if its == its_ref:
-            assert rel(host(x), x_ref) < (1e-10 if rel_tol < 1e-12 else 1e-7)
-        r = b - O.csr_vmult(rp, cols, vals, host(x))
-        assert abs(np.linalg.norm(r) - res) <= 1e-6 * np.linalg.norm(b)
+        # repeated solves: the round-1 defect (a scalar slot read and written
+        # in one kernel) showed up in some runs only
+        for _ in range(3):
+            x = torch.zeros(m.n_dofs, dtype=torch.float64, device="cuda")
+            its, res = sp.solve_cg(A, x, dev(b), preconditioner=precond, max_it=5000, abs_tol=abs_tol,
+                                   rel_tol=rel_tol)
+            assert abs(its - its_ref) <= 1, (its, its_ref)
+            if its == its_ref:
+                assert rel(host(x), x_ref) < (1e-10 if rel_tol < 1e-12 else 1e-7)
+            r = b - O.csr_vmult(rp, cols, vals, host(x))
+            assert abs(np.linalg.norm(r) - res) <= 1e-6 * np.linalg.norm(b)
 
 
 def test_cg_zero_rhs_and_no_convergence():
