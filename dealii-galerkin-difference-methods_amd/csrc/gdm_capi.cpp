@@ -100,6 +100,8 @@ struct gdm_op {
   double *yT1d = nullptr, *yT3d = nullptr, *m_yT3d = nullptr;  // v8 y corrections
   double sx8 = 0, cy8[19] = {0};
   double dint = 0, m_dint = 0;  // interior z scales of D (operator, mass)
+  double zd8[19] = {0}, m_zd8[19] = {0};  // dint * dhat[2p - k] (operator, mass)
+  int xcd_map = 1;
   int stencil_version = 8;
   int mass_version = 2;   // GDM_MASS=1: v1 in-place one-thread-per-line sweeps
   int mass_max_wgs = 0;   // GDM_MASS_WGS: cap on the line-solve grid (0 = all lines)
@@ -308,6 +310,7 @@ void build_tables(gdm_op *op) {
   op->sx = h[1] * beta[0];
   for (int k = 0; k < W; ++k) op->cy[k] = h[0] * beta[1] * bhat[k];
   op->m_dint = h[0] * h[1] * h[2];
+  for (int k = 0; k < W; ++k) op->m_zd8[k] = op->m_dint * mhat[2 * p - k];
   // v8 y tables: (wall row - Toeplitz row) corrections, column form; zero away
   // from the walls (the kernel adds them only for waves with wall rows)
   {
@@ -333,6 +336,7 @@ void build_tables(gdm_op *op) {
     op->zt8 = keep(op, dev_upload(z_table(&Mz8, Bz, 1.0, beta[2] * h[0] * h[1], bhat)));
     op->sx8 = op->sx * h[2];
     op->dint = beta[2] * h[0] * h[1];
+    for (int k = 0; k < W; ++k) op->zd8[k] = op->dint * bhat[2 * p - k];
     for (int k = 0; k < W; ++k) op->cy8[k] = op->cy[k] * h[2];
   }
   // mass operator tables for gdm_mass_apply on a non-mass op
@@ -553,14 +557,17 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
   gdmk_stencil8_geom(op->p, &ty8, &wgs8);
   const bool v8 = op->stencil_version == 8 && op->K[1] >= ty8 + 2 * op->p + 2 && op->K[0] >= 64 + 2 * op->p + 2;
   if (v8) a.yT1 = op->yT1d;
+  a.xcd_map = op->xcd_map;
   if (as_mass) {
     a.sx = 0.0;
     a.corrX = op->m_corrX;
     a.zt = op->m_zt;
     a.dint = op->m_dint;
+    for (int k = 0; k < 19; ++k) a.zd[k] = op->m_zd8[k];
     if (v8) a.yT3 = op->m_yT3d;
   } else if (v8) {
     a.dint = op->dint;
+    for (int k = 0; k < 19; ++k) a.zd[k] = op->zd8[k];
     a.sx = op->sx8;
     for (int k = 0; k < 19; ++k) a.cy[k] = op->cy8[k];
     a.corrX = op->corrX8;
@@ -745,6 +752,7 @@ int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int
   build_faces(op);
   op->zchunk = choose_zchunk(op);
   if (const char *env = std::getenv("GDM_STENCIL")) op->stencil_version = std::atoi(env) == 7 ? 7 : 8;
+  if (const char *env = std::getenv("GDM_XCD")) op->xcd_map = std::atoi(env) != 0;
   if (const char *env = std::getenv("GDM_MASS")) op->mass_version = std::atoi(env) == 1 ? 1 : 2;
   if (const char *env = std::getenv("GDM_MASS_WGS")) op->mass_max_wgs = std::max(0, std::atoi(env));
   hip_check(hipMalloc(&op->dot_partial, sizeof(double) * op->n_dot_partial), "hipMalloc");

@@ -43,6 +43,8 @@ struct StencilArgs {
   // out(zz - p + k) += mhat[k] E + dint dhat[2p - k] D, and zt's wall rows hold
   // (M_z / h_z, B_z) pairs.
   double dint;
+  double zd[19];  // v8 interior z column of D: dint * dhat[2p - k]
+  int xcd_map;    // v8: XCD-aware tile order (GDM_XCD=0 disables)
   // v8 only: output plane ranges computed by this launch (chunks of zchunk
   // planes; blockIdx.z < nchunk0 -> range 0, else range 1)
   int cz0[2], cz1[2], nchunk0;

@@ -533,12 +533,17 @@ struct Geom8 {
   static constexpr int NPASS = (NG + NP - 1) / NP;
   static constexpr int USZ = NG * 4 * RL;
   static constexpr int NAB = BK == 0 ? 1 : 2;
-  // (A, B) pairs: row stride 2 TX + 2 TX / 8 doubles with one pair of padding
-  // after every 8 x -- the producers' 4-pairs-per-lane ds_write_b128 stores
-  // then hit distinct banks; consumers read one pair per lane as before
-  static constexpr int ABRS = NAB == 2 ? 2 * TX + 2 * (TX / 8) : TX;
+  // (A, B) pairs: row stride 2 TX doubles, pair x stored in slot
+  // sw(x) = x ^ ((x >> 3) & 3).  Both access patterns are then bank-conflict
+  // free: the consumers' ds_read_b128 (one pair per lane, lane groups
+  // {0-3,12-15,20-27}, ... of MI355X_MICROARCH.md section LDS: 16 distinct
+  // 16-B slots of the 256-B bank row) and the producers' ds_write_b128 (lane q
+  // stores pairs 4q..4q+3; 8 contiguous lanes hit 8 distinct slots of 128 B).
+  // (The padded layout of v8 made the reads 2-way: 41 % of LDS cycles.)
+  static constexpr int ABRS = NAB == 2 ? 2 * TX : TX;
   static constexpr int ABSZ = UR * ABRS;
-  static __device__ __forceinline__ int ab(int r, int x) { return NAB == 2 ? r * ABRS + 2 * x + 2 * (x >> 3) : r * TX + x; }
+  static __device__ __forceinline__ int sw(int x) { return x ^ ((x >> 3) & 3); }
+  static __device__ __forceinline__ int ab(int r, int x) { return NAB == 2 ? r * ABRS + 2 * sw(x) : r * TX + x; }
   static constexpr int ZTSZ = (2 * W + 1) * W * 2;  // wall planes + interior row
   static constexpr int YCSZ = UR * W * 2;
   static constexpr int CORRSZ = 2 * (P + 1) * 2 * W;
@@ -610,7 +615,10 @@ __device__ __forceinline__ void xsweep8(const StencilArgs &a, const Tile7 &t, lc
             V[j / 2].y = fma(IR::m[k], w[j + k + 1], V[j / 2].y);
         } else {
           V[j].x = fma(IR::m[k], w[j + k + 1], V[j].x);
-          if constexpr (BK == 1) V[j].y = fma(IR::c[k], w[j + k + 1], V[j].y);
+          // the antisymmetric interior band has c[p] == 0: no FMA for it
+          if constexpr (BK == 1) {
+            if (IR::c[k] != 0.0) V[j].y = fma(IR::c[k], w[j + k + 1], V[j].y);
+          }
           if constexpr (BK == 2) V[j].y = fma(IR::l[k], w[j + k + 1], V[j].y);
         }
       }
@@ -680,9 +688,11 @@ __device__ __forceinline__ void write_ab8(const Tile7 &t, int g, const dpair (&V
   const int r = 4 * g + rr;
   if (r < G::UR) {
     if constexpr (BK != 0) {
-      ldouble2 *p = (ldouble2 *)(t.ab0 + G::ab(r, 4 * q));  // 4 q .. 4 q + 3 share one 8-x block
+      // sw(4q + j) = 4q + (j ^ t), t = (q >> 1) & 3: the lane's 4 pairs stay in its 4-pair block
+      ldouble2 *p = (ldouble2 *)(t.ab0 + r * G::ABRS + 8 * q);
+      const int tq = (q >> 1) & 3;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) p[j] = V[j];
+      for (int j = 0; j < 4; ++j) p[j ^ tq] = V[j];
     } else {
       ldouble2 *p = (ldouble2 *)(t.ab0 + r * TX + 4 * q);
       p[0] = V[0];
@@ -830,7 +840,10 @@ __device__ __forceinline__ void ysweep8(const StencilArgs &a, const Tile7 &t, do
         const int k = s - j;  // row form: M(y_j, y_j - p + k)
         if (k >= 0 && k < W) {
           D[j] = fma(IR::m[k], v[s].x, D[j]);
-          E[j] = fma(IR::m[k], v[s].y, fma(a.cy[k], v[s].x, E[j]));
+          if (BK == 1 && k == P)  // cy[p] = h_x a_y chat[p] = 0
+            E[j] = fma(IR::m[k], v[s].y, E[j]);
+          else
+            E[j] = fma(IR::m[k], v[s].y, fma(a.cy[k], v[s].x, E[j]));
         }
       }
     }
@@ -887,8 +900,8 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
     GDM_LDS_BARRIER();  // F_i+1
     if (!GDM_DBG(a, 2)) {
       if constexpr (!WALL) {
-#pragma unroll
-        for (int j = 0; j < R; ++j) D[j] *= a.dint;
+        // interior z column: out += mhat[k] E + zd[k] D with zd = dint dhat[2p - k]
+        // (the scale folded into the coefficients; zd[p] = 0 for advection)
 #pragma unroll
         for (int k = 0; k < W; ++k) {
           GDM_FENCE();
@@ -896,9 +909,11 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
 #pragma unroll
           for (int j = 0; j < R; ++j) {
             if constexpr (BK == 0)
-              acc[slot][j] = fma(zband<P, BK>(k), D[j], acc[slot][j]);
+              acc[slot][j] = fma(a.zd[k], D[j], acc[slot][j]);
+            else if (zband<P, BK>(k) == 0.0)
+              acc[slot][j] = fma(IR::m[k], E[j], acc[slot][j]);
             else
-              acc[slot][j] = fma(IR::m[k], E[j], fma(zband<P, BK>(k), D[j], acc[slot][j]));
+              acc[slot][j] = fma(IR::m[k], E[j], fma(a.zd[k], D[j], acc[slot][j]));
           }
         }
       } else {
@@ -1021,16 +1036,30 @@ __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, N
   t.yw = lds + G::OFF_YW;
   t.lane = threadIdx.x & 63;
   t.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  t.x0 = blockIdx.x * G::TX;
-  t.y0 = a.out_y0 + blockIdx.y * G::TY;
+  // XCD-aware tile order: the hardware deals workgroup b to XCD b % 8; XCD k
+  // gets the contiguous logical range [k q, (k + 1) q) of tiles (x fastest),
+  // so the tiles sharing x- and y-halo lines run on one XCD at the same time
+  // and those lines are fetched from HBM once into that XCD's L2.
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (a.xcd_map) {
+    const int64_t gx = gridDim.x, gy = gridDim.y;
+    const int64_t nb = gx * gy * gridDim.z, q = nb / 8;
+    const int64_t b = blockIdx.x + gx * (blockIdx.y + gy * (int64_t)blockIdx.z);
+    const int64_t L = b >= 8 * q ? b : (b % 8) * q + b / 8;
+    bx = (int)(L % gx);
+    by = (int)((L / gx) % gy);
+    bz = (int)(L / (gx * gy));
+  }
+  t.x0 = bx * G::TX;
+  t.y0 = a.out_y0 + by * G::TY;
 #ifdef GDM_EXP_NOY
   t.yedge = false;  // timing experiment: wrong next to the y walls
 #else
   t.yedge = ywall_begin<P, G::TY>(a, t.y0) >= 0;
 #endif
   {
-    const int r = (int)blockIdx.z < a.nchunk0 ? 0 : 1;
-    const int c = (int)blockIdx.z - (r ? a.nchunk0 : 0);
+    const int r = bz < a.nchunk0 ? 0 : 1;
+    const int c = bz - (r ? a.nchunk0 : 0);
     t.zc0 = a.cz0[r] + c * a.zchunk;
     t.zc1 = min(t.zc0 + a.zchunk, a.cz1[r]);
   }
