@@ -103,11 +103,17 @@ struct gdm_op {
   double zd8[19] = {0}, m_zd8[19] = {0};  // dint * dhat[2p - k] (operator, mass)
   int xcd_map = 1;
   int stencil_version = 8;
-  int mass_version = 2;   // GDM_MASS=1: v1 in-place one-thread-per-line sweeps
+  int mass_version = 3;   // GDM_MASS=1: v1 in-place one-thread-per-line sweeps, 2: v2 two-sweep lines
   int mass_max_wgs = 0;   // GDM_MASS_WGS: cap on the line-solve grid (0 = all lines)
   // the same for the mass operator of an advection/wave op (gdm_mass_apply)
   double *m_corrX = nullptr, *m_zt = nullptr;
   double *lrow[3] = {nullptr, nullptr, nullptr}, *invd[3] = {nullptr, nullptr, nullptr};
+  // mass inverse v3 tables (gdm_mass.hip): [rows][p] lower / upper factor rows,
+  // inverse diagonal, the interior fixed-point row and its row range
+  double *l3[3] = {nullptr, nullptr, nullptr}, *u3[3] = {nullptr, nullptr, nullptr}, *d3[3] = {nullptr, nullptr, nullptr};
+  double *cst3[3] = {nullptr, nullptr, nullptr};
+  int row_lo3[3] = {0, 0, 0}, row_hi3[3] = {0, 0, 0};
+  std::vector<double> cst3_host[3];
   std::vector<Face> faces;
   double *face_tmp = nullptr;
   int64_t face_tmp_size = 0;
@@ -353,6 +359,44 @@ void build_tables(gdm_op *op) {
     lrow.resize(lrow.size() + (size_t)p * (p + 1), 0.0);  // zero pad for the backward sweep
     op->lrow[ax] = keep(op, dev_upload(lrow));
     op->invd[ax] = keep(op, dev_upload(invd));
+    // v3: split rows, zero-padded by 3C + p rows past the line end
+    const int C3 = gdmk_mass3_chunk(p);
+    if (C3 > 0) {
+      const int n = M[ax].n, rows = n + 3 * C3 + p;
+      const int wl = p + 1;
+      std::vector<double> l3((size_t)rows * p, 0.0), u3((size_t)rows * p, 0.0), d3((size_t)rows, 0.0);
+      for (int i = 0; i < n; ++i) {
+        for (int k = 0; k < p; ++k) l3[(size_t)i * p + k] = lrow[(size_t)i * wl + k] * invd[i];
+        for (int m = 1; m <= p; ++m)
+          if (i + m < n) u3[(size_t)i * p + m - 1] = lrow[(size_t)(i + m) * wl + (p - m)] * invd[i];
+        d3[i] = invd[i];
+      }
+      // the run of rows around the middle that equal the middle row bitwise
+      const int mid = n / 2;
+      auto same = [&](int i) {
+        if (d3[i] != d3[mid]) return false;
+        for (int k = 0; k < p; ++k)
+          if (l3[(size_t)i * p + k] != l3[(size_t)mid * p + k] || u3[(size_t)i * p + k] != u3[(size_t)mid * p + k])
+            return false;
+        return true;
+      };
+      int lo = mid, hi = mid + 1;
+      while (lo > 0 && same(lo - 1)) --lo;
+      while (hi < n && same(hi)) ++hi;
+      std::vector<double> cst(2 * p + 1);
+      for (int k = 0; k < p; ++k) {
+        cst[k] = l3[(size_t)mid * p + k];
+        cst[p + k] = u3[(size_t)mid * p + k];
+      }
+      cst[2 * p] = d3[mid];
+      op->l3[ax] = keep(op, dev_upload(l3));
+      op->u3[ax] = keep(op, dev_upload(u3));
+      op->d3[ax] = keep(op, dev_upload(d3));
+      op->cst3[ax] = keep(op, dev_upload(cst));  // device copy unused by the kernels; host copy below
+      op->cst3_host[ax] = cst;
+      op->row_lo3[ax] = lo;
+      op->row_hi3[ax] = hi;
+    }
   }
 }
 
@@ -753,7 +797,7 @@ int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int
   op->zchunk = choose_zchunk(op);
   if (const char *env = std::getenv("GDM_STENCIL")) op->stencil_version = std::atoi(env) == 7 ? 7 : 8;
   if (const char *env = std::getenv("GDM_XCD")) op->xcd_map = std::atoi(env) != 0;
-  if (const char *env = std::getenv("GDM_MASS")) op->mass_version = std::atoi(env) == 1 ? 1 : 2;
+  if (const char *env = std::getenv("GDM_MASS")) op->mass_version = std::max(1, std::min(3, std::atoi(env)));
   if (const char *env = std::getenv("GDM_MASS_WGS")) op->mass_max_wgs = std::max(0, std::atoi(env));
   hip_check(hipMalloc(&op->dot_partial, sizeof(double) * op->n_dot_partial), "hipMalloc");
   keep(op, op->dot_partial);
@@ -866,24 +910,28 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
                                        op->stream), "chol x");
     return GDM_OK;
   }
-  // v2 (gdm_mass.hip): the first pass reads rhs and writes x, later passes in place
+  // v3 (gdm_mass.hip, single sweep per direction) where supported, else v2
+  // (two sweeps); the first pass reads rhs and writes x, later passes in place
   const double *in = rhs_owned;
   const int wg = op->mass_max_wgs;
-  if (Z > 1) {  // z lines: (x, y) -> base = l, step X*Y
-    hip_check(gdmk_launch_mass_lines(op->p, 1, in, x_owned, (int)Z, X * Y, X * Y, X * Y, 0, op->lrow[2], op->invd[2],
-                                     wg, op->stream), "mass z");
+  const bool v3 = op->mass_version >= 3 && gdmk_mass3_chunk(op->p) > 0;
+  auto pass = [&](int ax, int dir_kind, int64_t len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,
+                  const char *what) {
+    const bool aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(x_owned)) & 15) == 0;
+    if (v3 && op->l3[ax] && (dir_kind == 1 || (len % 2 == 0 && aligned)))
+      hip_check(gdmk_launch_mass3(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, op->l3[ax],
+                                  op->u3[ax], op->d3[ax], op->cst3_host[ax].data(), op->row_lo3[ax], op->row_hi3[ax],
+                                  op->stream),
+                what);
+    else
+      hip_check(gdmk_launch_mass_lines(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, op->lrow[ax],
+                                       op->invd[ax], wg, op->stream),
+                what);
     in = x_owned;
-  }
-  if (Y > 1) {  // y lines: (x, z) -> base = z*X*Y + x, step X
-    hip_check(gdmk_launch_mass_lines(op->p, 1, in, x_owned, (int)Y, X, X * Z, X, X * Y, op->lrow[1], op->invd[1], wg,
-                                     op->stream), "mass y");
-    in = x_owned;
-  }
-  if (X > 1) {  // x lines: contiguous rows of length X
-    hip_check(gdmk_launch_mass_lines(op->p, 0, in, x_owned, (int)X, 1, Y * Z, 1, 0, op->lrow[0], op->invd[0], wg,
-                                     op->stream), "mass x");
-    in = x_owned;
-  }
+  };
+  if (Z > 1) pass(2, 1, Z, X * Y, X * Y, X * Y, 0, "mass z");   // z lines: (x, y) -> base = l, step X*Y
+  if (Y > 1) pass(1, 1, Y, X, X * Z, X, X * Y, "mass y");       // y lines: (x, z) -> base = z*X*Y + x, step X
+  if (X > 1) pass(0, 0, X, 1, Y * Z, 1, 0, "mass x");           // x lines: contiguous rows of length X
   if (in != x_owned)
     hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
   return GDM_OK;

@@ -91,6 +91,12 @@ hipError_t gdmk_launch_chol_lines(int p, double *v, int len, int64_t stride, int
 hipError_t gdmk_launch_mass_lines(int p, int dir_kind, const double *src, double *dst, int len, int64_t stride,
                                   int64_t n_lines, int64_t A, int64_t B, const double *lrow, const double *inv_diag,
                                   int max_wgs, hipStream_t st);
+// mass inverse v3 single-sweep line solves (gdm_mass.hip); chunk length C(p)
+// (0 = unsupported degree); tables padded with zero rows to len + 3 C + p
+int gdmk_mass3_chunk(int p);
+hipError_t gdmk_launch_mass3(int p, int dir_kind, const double *src, double *dst, int len, int64_t stride,
+                             int64_t n_lines, int64_t A, int64_t B, const double *lrow, const double *urow,
+                             const double *invd, const double *cst, int row_lo, int row_hi, hipStream_t st);
 hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st);
 hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st);
 hipError_t gdmk_launch_dot(int64_t n, const double *x, const double *y, double *partial, int n_partial, double *out,

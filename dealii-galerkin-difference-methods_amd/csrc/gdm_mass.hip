@@ -31,6 +31,13 @@
 
 namespace gdmk {
 
+#define GDM_WAIT_VMCNT(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
+// wave-uniform coefficient reads through the constant address space (scalar loads)
+typedef __attribute__((address_space(4))) const double cdouble;
+__device__ __forceinline__ cdouble *cptr(const double *p) { return (cdouble *)(p); }
+typedef double dpair __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) dpair ldouble2;
+
 namespace {
 
 // factor rows: lrow[i * (P + 1) + k] = L(i, i - P + k), k = P is the diagonal;
@@ -244,6 +251,358 @@ __global__ void __launch_bounds__(64) chol_rows_kernel(const double *src, double
   }
 }
 
+// ===========================================================================
+// v3: single-sweep line solves, 16 B/DoF per direction.
+//
+// The forward factor L^-1 and the backward factor L^-T are stable recurrences
+// whose homogeneous solutions decay below 1e-16 (relative) within C positions
+// (the impulse response of the p = 5 GDM mass factor drops below 1e-17 after
+// 50 positions, p = 7 after 57).  A line is therefore marched
+// ONCE: the forward values of two consecutive chunks live in a register ring
+// (2 x C doubles, compile-time indices), and as soon as chunk c is
+// forward-solved, chunk c-1 is back-solved, the backward recurrence starting
+// from a zero state at the end of chunk c (a warm-up over chunk c whose values
+// are not kept): its initial-state error has decayed below 1e-16 by the time
+// it reaches chunk c-1.  The last chunk of a line is back-solved from the true
+// (zero) end state.  Every value is read once and written once.
+//
+// Coefficient tables (wave-uniform positions -> scalar loads), padded with zero
+// rows past the line end so positions >= len produce exact zeros, prescaled by
+// the inverse diagonal so each position's dependence on its predecessor is a
+// single FMA:
+//   lrow[i][k] = L(i, i - P + k) / L(i, i), k < P;  urow[i][m - 1] = L(i + m, i) / L(i, i);
+//   invd[i] = 1 / L(i, i)
+// The Cholesky rows reach a fixed point a few dozen rows into the line and keep
+// it until the last p rows; chunks inside that range take the coefficients
+// from kernel arguments (SGPRs) instead.
+template <int P>
+struct Cst3 {
+  double l[P], u[P], d;
+  int row_lo, row_hi;  // rows [row_lo, row_hi) of lrow / invd, [row_lo, row_hi - P) of urow equal l, d, u
+};
+
+template <int P>
+struct Geo3 {
+  static constexpr int C = P <= 5 ? 48 : 56;  // chunk = warm-up length
+  // strided: loads in flight per lane.  One chunk ahead: with the 2C-double
+  // ring this runs one wave per SIMD, so the FIFO alone must cover the HBM
+  // latency (Q * 512 B per wave; a 16-deep FIFO measured as latency-bound)
+  static constexpr int Q = P <= 5 ? C : C / 2;  // p = 7: 28 (one full chunk spills)
+  static constexpr int QL = 4;                // rows: LDS pair reads ahead
+  static constexpr int UPR = (C + 2) / 2;     // rows: 16-B units per LDS row (pitch C + 2 doubles)
+  static constexpr int TILE = 64 * UPR;       // rows: units per tile (= 64 x DMA instructions)
+  static constexpr size_t lds_bytes() { return 2 * (size_t)TILE * 16; }
+  static_assert(C % Q == 0 && C % 4 == 0, "chunk geometry");
+};
+
+// compiler-only fence: the scheduler may not move instructions across it
+#define GDM_FENCE()                    \
+  do {                                 \
+    asm volatile("" ::: "memory");     \
+    __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
+template <int P>
+struct Ring3 {
+  static constexpr int C = Geo3<P>::C;
+  cdouble *L, *U, *D;
+  const Cst3<P> &k;
+
+  template <bool TAB>
+  __device__ __forceinline__ double lco(int i, int q) const {
+    if constexpr (TAB) return L[(size_t)i * P + q]; else return k.l[q];
+  }
+  template <bool TAB>
+  __device__ __forceinline__ double uco(int i, int q) const {
+    if constexpr (TAB) return U[(size_t)i * P + q]; else return k.u[q];
+  }
+  template <bool TAB>
+  __device__ __forceinline__ double dco(int i) const {
+    if constexpr (TAB) return D[i]; else return k.d;
+  }
+  // table mode: the row index of every group of 4 positions passes through an
+  // opaque SGPR move, so the (invariant, scalar) coefficient loads cannot be
+  // hoisted over the whole chunk (that spills hundreds of SGPRs)
+  template <bool TAB>
+  __device__ __forceinline__ int grp(int i) const {
+    if constexpr (TAB) asm volatile("" : "+s"(i));
+    return i;
+  }
+
+  // cur <- w of the chunk at base (b values from get(j), j chunk-local and
+  // compile-time, increasing); prev = w of the previous chunk (zeros before
+  // the line start)
+  template <bool TAB, class Get>
+  __device__ __forceinline__ void fwd(double (&cur)[C], const double (&prev)[C], int base, Get &&get) const {
+    int ib = base;
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      if (j % 4 == 0) {
+        GDM_FENCE();
+        ib = grp<TAB>(base + j) - j;
+      }
+      const int i = ib + j;
+      double s = get(j) * dco<TAB>(i);
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        const int jj = j - P + q;
+        s = fma(-lco<TAB>(i, q), jj >= 0 ? cur[jj] : prev[C + jj], s);
+      }
+      cur[j] = s;
+    }
+    GDM_FENCE();
+  }
+  // out: w on entry, x on exit (positions base .. base + C - 1).  WARM: start
+  // the recurrence from zero at base + 2C - 1 and run it over `next` (the
+  // following chunk's w, not modified); otherwise the state after the chunk is
+  // zero (line end).
+  template <bool WARM, bool TAB>
+  __device__ __forceinline__ void bwd(double (&out)[C], const double (&next)[C], int base) const {
+    double t[P];  // x at positions base + C + q, slot q % P
+#pragma unroll
+    for (int q = 0; q < P; ++q) t[q] = 0.0;
+    if constexpr (WARM) {
+      int ib = base + C;
+#pragma unroll
+      for (int q = C - 1; q >= 0; --q) {
+        if ((C - 1 - q) % 4 == 0) ib = grp<TAB>(base + C + q) - q;
+        const int i = ib + q;
+        double s = next[q] * dco<TAB>(i);
+#pragma unroll
+        for (int m = P; m >= 1; --m)
+          if (q + m < C) s = fma(-uco<TAB>(i, m - 1), t[(q + m) % P], s);
+        t[q % P] = s;
+      }
+    }
+    int ib = base;
+#pragma unroll
+    for (int j = C - 1; j >= 0; --j) {
+      if ((C - 1 - j) % 4 == 0) ib = grp<TAB>(base + j) - j;
+      const int i = ib + j;
+      double s = out[j] * dco<TAB>(i);
+#pragma unroll
+      for (int m = P; m >= 1; --m) {
+        const int jj = j + m;
+        s = fma(-uco<TAB>(i, m - 1), jj < C ? out[jj] : t[(jj - C) % P], s);
+      }
+      out[j] = s;
+    }
+    GDM_FENCE();
+  }
+  // one march step: forward chunk c into cur, then back-solve chunk c - 1
+  // (prev) with the warm-up over cur
+  template <class Get>
+  __device__ __forceinline__ void step(double (&cur)[C], double (&prev)[C], int c, Get &&get) const {
+    const int base = c * C;
+    if (base - C >= k.row_lo && base + C + P <= k.row_hi - P) {
+      fwd<false>(cur, prev, base, get);
+      bwd<true, false>(prev, cur, base - C);
+    } else {
+      fwd<true>(cur, prev, base, get);
+      bwd<true, true>(prev, cur, base - C);
+    }
+  }
+};
+
+// Strided lines: lane = line, line l -> base (l / A) * B + l % A, step stride
+// (consecutive lanes = consecutive addresses: every load / store instruction
+// moves one contiguous 512-B row segment).  The loads stream Q positions ahead
+// of the forward recurrence through a register FIFO, across chunk borders.
+// Requires (len - 1) * stride + 64 entries to span < 2^31 bytes... (host-checked:
+// the offsets are 64-bit SGPR values, the lane offset is 32-bit).  src may
+// equal dst.
+template <int P>
+__global__ void __launch_bounds__(64) mass3_strided_kernel(const double *src, double *dst, int len, int64_t stride,
+                                                           int64_t n_lines, int64_t A, int64_t B,
+                                                           const double *__restrict__ lrow,
+                                                           const double *__restrict__ urow,
+                                                           const double *__restrict__ invd, const Cst3<P> k) {
+  using R = Ring3<P>;
+  constexpr int C = R::C, Q = Geo3<P>::Q;
+  const R r{cptr(lrow), cptr(urow), cptr(invd), k};
+  // lanes past n_lines repeat the last line (same values, same addresses)
+  const int64_t line = min((int64_t)blockIdx.x * 64 + threadIdx.x, n_lines - 1);
+  // wave-uniform base (lane 0's line) + a 32-bit lane byte offset: one SGPR
+  // address + one shared offset VGPR per access (global_load saddr form)
+  const int64_t b0 = (line / A) * B + (line % A);
+  const int64_t bw = ((int64_t)__builtin_amdgcn_readfirstlane((int)(b0 >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b0);
+  const uint32_t lbyte = (uint32_t)(b0 - bw) * 8u;
+  // the uniform byte offset of a position passes through an opaque SGPR move,
+  // or LICM hoists every per-position address out of the march loop
+  auto at = [&](const double *v, int i) -> const double & {
+    int64_t o = (int64_t)i * stride * 8;
+    asm volatile("" : "+s"(o));
+    return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(v + bw) + o + lbyte);
+  };
+  double fifo[Q];
+  int cb = 0;  // base of the chunk being forward-solved
+  auto get = [&](int j) -> double {
+    const double b = fifo[j % Q];
+    fifo[j % Q] = at(src, min(cb + j + Q, len - 1));
+    return b;
+  };
+  auto store = [&](const double (&h)[C], int base) {
+    if (base + C <= len) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        if (j % 8 == 0) GDM_FENCE();
+        const_cast<double &>(at(dst, base + j)) = h[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < C; ++j)
+        if (base + j < len) const_cast<double &>(at(dst, base + j)) = h[j];
+    }
+    GDM_FENCE();
+  };
+  double h0[C], h1[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) h1[j] = 0.0;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) fifo[q] = at(src, min(q, len - 1));
+  r.template fwd<true>(h0, h1, 0, get);
+  for (int c = 1;; c += 2) {
+    if (c * C >= len) {
+      r.template bwd<false, true>(h0, h1, (c - 1) * C);
+      store(h0, (c - 1) * C);
+      break;
+    }
+    cb = c * C;
+    r.step(h1, h0, c, get);
+    store(h0, (c - 1) * C);
+    if ((c + 1) * C >= len) {
+      r.template bwd<false, true>(h1, h0, c * C);
+      store(h1, c * C);
+      break;
+    }
+    cb = (c + 1) * C;
+    r.step(h0, h1, c + 1, get);
+    store(h1, c * C);
+  }
+}
+
+// Contiguous lines (x): one wave owns 64 consecutive lines; chunk c of all 64
+// lines (64 rows x C doubles) is staged by LDS-DMA (16 B per lane, the
+// row-coalesced image of the rows, pitch C + 2 doubles: conflict-free
+// ds_read_b128 of a lane's own row) one chunk ahead into tile c % 2; the
+// back-solved chunk is written into the tile just consumed and stored
+// row-coalesced.  Every lane issues every store (invalid lanes repeat a valid
+// lane's store with the same data), so the counted vmcnt is exact.
+// Requires len even and 16-B aligned src / dst (host-checked).
+template <int P>
+__global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, double *dst, int len, int64_t n_lines,
+                                                        const double *__restrict__ lrow,
+                                                        const double *__restrict__ urow,
+                                                        const double *__restrict__ invd, const Cst3<P> k) {
+  using R = Ring3<P>;
+  using G = Geo3<P>;
+  constexpr int C = R::C, UPR = G::UPR, QL = G::QL;
+  extern __shared__ __attribute__((aligned(16))) char smem3[];
+  ldouble2 *tile0 = (ldouble2 *)smem3;
+  ldouble2 *tile1 = tile0 + G::TILE;
+  const R r{cptr(lrow), cptr(urow), cptr(invd), k};
+  const int lane = threadIdx.x;
+  const int64_t l0 = (int64_t)blockIdx.x * 64;
+  const int nl = (int)min<int64_t>(64, n_lines - l0);
+  __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(src + l0 * len), 0, (int)((int64_t)nl * len * 8), 0x00020000);
+  double *dbase = dst + l0 * len;
+
+  // the lane index passes through an opaque VGPR move in the helpers below:
+  // otherwise LICM keeps every per-instruction (row, pair) offset of the DMA
+  // and the stores live across the march loop (~100 VGPRs)
+  auto dma = [&](ldouble2 *t, int base) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int q = 0; q < UPR; ++q) {
+      const int u = q * 64 + ln, row = u / UPR, pair = u - row * UPR;
+      const uint32_t voff = (uint32_t)(((int64_t)row * len + base + 2 * pair) * 8);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(t + q * 64), 16,
+                                               voff, 0, 0, 0);
+    }
+  };
+  // b values of the lane's row, read QL pairs ahead from the tile
+  dpair fl[QL];
+  const ldouble2 *trow = tile0;
+  auto get = [&](int j) -> double {
+    const dpair v = fl[(j / 2) % QL];
+    if (j % 2 == 1 && j / 2 + QL < C / 2) fl[(j / 2) % QL] = trow[j / 2 + QL];
+    return j % 2 ? v.y : v.x;
+  };
+  auto open_row = [&](const ldouble2 *t) {
+    trow = t + lane * UPR;
+#pragma unroll
+    for (int q = 0; q < QL; ++q) fl[q] = trow[q];
+  };
+  auto write_row = [&](ldouble2 *t, const double (&h)[C]) {
+#pragma unroll
+    for (int jp = 0; jp < C / 2; ++jp) {
+      dpair v;
+      v.x = h[2 * jp];
+      v.y = h[2 * jp + 1];
+      t[lane * UPR + jp] = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto store = [&](const ldouble2 *t, int base) {
+    const int last_pair = min(C / 2, (len - base) / 2) - 1;  // >= 0: base < len, len even
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int q = 0; q < UPR; ++q) {
+      if (q % 6 == 0) GDM_FENCE();
+      const int u = q * 64 + ln;
+      const int row = min(u / UPR, nl - 1), pair = min(u % UPR, last_pair);
+      const dpair v = t[row * UPR + pair];
+      *reinterpret_cast<dpair *>(dbase + (int64_t)row * len + base + 2 * pair) = v;
+    }
+    GDM_FENCE();
+  };
+
+  double h0[C], h1[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) h1[j] = 0.0;
+  dma(tile0, 0);
+  GDM_WAIT_VMCNT(0);
+  if (C < len) dma(tile1, C);
+  open_row(tile0);
+  r.template fwd<true>(h0, h1, 0, get);
+  for (int c = 1;; c += 2) {
+    // ---- chunk c (odd): tile1, ring h1; chunk c - 1 in h0 (its input tile0 is free) ----
+    if (c * C >= len) {
+      r.template bwd<false, true>(h0, h1, (c - 1) * C);
+      write_row(tile0, h0);
+      store(tile0, (c - 1) * C);
+      break;
+    }
+    if (c == 1)
+      GDM_WAIT_VMCNT(0);  // only DMA(1) is in flight
+    else
+      GDM_WAIT_VMCNT(UPR);  // DMA(c) retired; the stores issued after it may be in flight
+    if ((c + 1) * C < len) dma(tile0, (c + 1) * C);
+    open_row(tile1);
+    r.step(h1, h0, c, get);
+    write_row(tile1, h0);
+    store(tile1, (c - 1) * C);
+    // ---- chunk c + 1 (even): tile0, ring h0; chunk c in h1 ----
+    if ((c + 1) * C >= len) {
+      r.template bwd<false, true>(h1, h0, c * C);
+      write_row(tile1, h1);
+      store(tile1, c * C);
+      break;
+    }
+    GDM_WAIT_VMCNT(UPR);
+    if ((c + 2) * C < len) dma(tile1, (c + 2) * C);
+    open_row(tile0);
+    r.step(h0, h1, c + 1, get);
+    write_row(tile0, h1);
+    store(tile0, c * C);
+  }
+  GDM_WAIT_VMCNT(0);
+}
+
 namespace {
 
 template <int P>
@@ -268,9 +627,66 @@ hipError_t launch_mass_lines_p(int dir_kind, const double *src, double *dst, int
   return hipGetLastError();
 }
 
+template <int P>
+hipError_t launch_mass3_p(int dir_kind, const double *src, double *dst, int len, int64_t stride, int64_t n_lines,
+                          int64_t A, int64_t B, const double *lrow, const double *urow, const double *invd,
+                          const double *cst, int row_lo, int row_hi, hipStream_t st) {
+  Cst3<P> k;
+  for (int q = 0; q < P; ++q) {
+    k.l[q] = cst[q];
+    k.u[q] = cst[P + q];
+  }
+  k.d = cst[2 * P];
+  k.row_lo = row_lo;
+  k.row_hi = row_hi;
+  const unsigned grid = (unsigned)((n_lines + 63) / 64);
+  if (dir_kind == 0) {
+    const size_t lds = Geo3<P>::lds_bytes();
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mass3_rows_kernel<P>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(mass3_rows_kernel<P>, dim3(grid), dim3(64), lds, st, src, dst, len, n_lines, lrow, urow, invd, k);
+  } else {
+    hipLaunchKernelGGL(mass3_strided_kernel<P>, dim3(grid), dim3(64), 0, st, src, dst, len, stride, n_lines, A, B,
+                       lrow, urow, invd, k);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 }  // namespace gdmk
+
+// v3 single-sweep line solves.  Tables: lrow [rows][p], urow [rows][p], invd
+// [rows], rows >= len + 3 C + p with zero rows from len on; cst = the interior
+// row (l[p], u[p], d) that rows [row_lo, row_hi) (urow: [row_lo, row_hi - p))
+// hold exactly.
+// dir_kind 0 (contiguous lines) requires len even and 16-B aligned src / dst.
+extern "C" int gdmk_mass3_chunk(int p) {
+  switch (p) {
+    case 3: return gdmk::Geo3<3>::C;
+    case 5: return gdmk::Geo3<5>::C;
+    case 7: return gdmk::Geo3<7>::C;
+    default: return 0;
+  }
+}
+extern "C" hipError_t gdmk_launch_mass3(int p, int dir_kind, const double *src, double *dst, int len, int64_t stride,
+                                       int64_t n_lines, int64_t A, int64_t B, const double *lrow, const double *urow,
+                                       const double *invd, const double *cst, int row_lo, int row_hi,
+                                       hipStream_t st) {
+  using namespace gdmk;
+  if (n_lines <= 0 || len <= 0) return hipSuccess;
+  switch (p) {
+    case 3: return launch_mass3_p<3>(dir_kind, src, dst, len, stride, n_lines, A, B, lrow, urow, invd, cst, row_lo, row_hi, st);
+    case 5: return launch_mass3_p<5>(dir_kind, src, dst, len, stride, n_lines, A, B, lrow, urow, invd, cst, row_lo, row_hi, st);
+    case 7: return launch_mass3_p<7>(dir_kind, src, dst, len, stride, n_lines, A, B, lrow, urow, invd, cst, row_lo, row_hi, st);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 // dir_kind 0: contiguous lines (line l at l * len, stride 1);
 // dir_kind 1: strided lines, base = (l / A) * B + (l % A), step `stride`.

@@ -169,6 +169,38 @@ def test_mass_solve_ragged_vs_kron(shape, p, in_place):
     assert rel(host(x), ref) < 1e-12
 
 
+@pytest.mark.parametrize("shape", [(499, 7, 8), (7, 433, 8), (7, 8, 601), (239, 190), (1023, 7), (8, 7, 145)])
+@pytest.mark.parametrize("p", [3, 5, 7])
+def test_mass_solve_v3_long_lines(shape, p):
+    """Mass inverse v3 (single-sweep line solves with the truncated backward
+    warm-up, gdm_mass.hip) on lines of many chunks (C = 48 / 56 positions),
+    lengths that are not chunk multiples, both the table and the interior
+    fixed-point coefficient paths: against the exact Kronecker inverse and,
+    element-wise, against the two-sweep v2 solve."""
+    import os
+
+    g = _gdm()
+    dim = len(shape)
+    lo, hi = (0.0,) * dim, (1.0, 0.7, 1.3)[:dim]
+    m = O.Mesh(dim, p, list(shape), lo, hi)
+    r = np.random.default_rng(33).uniform(-1, 1, m.n_dofs)
+    ref = m.kron_mass_inverse(r)
+    out = {}
+    for ver in ("3", "2"):
+        os.environ["GDM_MASS"] = ver
+        try:
+            op = g.GdmOperator(dim, p, shape, lo, hi, "mass")
+        finally:
+            del os.environ["GDM_MASS"]
+        x = op.new_vector(local=False)
+        op.mass_solve(dev(r), x)
+        out[ver] = host(x)
+        del op
+    assert rel(out["3"], ref) < 1e-12
+    scale = np.max(np.abs(out["2"]))
+    assert np.max(np.abs(out["3"] - out["2"])) < 1e-13 * scale
+
+
 @pytest.mark.parametrize("shape", [(70, 33, 20), (64, 64, 64), (131, 5, 9), (5, 5, 100), (150, 90, 70), (97, 61, 130)])
 @pytest.mark.parametrize("p", [5, 7])
 def test_ragged_3d_vs_kron(shape, p):
