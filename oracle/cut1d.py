@@ -1,0 +1,387 @@
+"""1D cut-cell GDM restatement of the reference's wave application (test
+infrastructure: only tests/ may import it).
+
+Restates, for dim = 1, what applications/wave computes (paths relative to the
+reference root):
+
+  * mesh + categories + DoF boxes      include/gdm/system.h:195-246, 404-424
+  * level set: FE_Q(p) interpolant of SignedDistance::Sphere (|x| - r),
+    MeshClassifier (inside / outside / intersected)
+                                       applications/wave/include/gdm/wave/discretization.h:82-99
+  * NonMatching::FEValues in 1D: QGauss(p+1) on the inside part of a cut
+    cell, one surface point at the root with weight 1 and the level-set
+    normal
+  * mass matrix  (v, u)_inside + 0.5 g_M h^3 [dv/dn][du/dn] on ghost-penalty
+    faces, zero diagonals -> 1      .../wave/mass.h:47-249
+  * compute_rhs: -(v', u') + (v, f) + surface Nitsche (gamma_D = 5p) +
+    -0.5 g_A h [v'][u'] (GP, h^1 in the rhs)   .../wave/stiffness.h:42-407
+  * stiffness matrix: (v', u') + surface Nitsche + 0.5 g_A h^3 [v'][u']
+    (GP, h^3 in the matrix)          .../wave/stiffness.h:602-800
+  * wave-rk, heat-rk (RK_CLASSIC_FOURTH_ORDER + DiscreteTime), heat-impl
+    (u <- (M + dt S)^-1 (M u + dt f))  .../wave/problem.h:39-346
+  * postprocess: L2 / L1 / Linf error on the inside quadrature
+                                       .../wave/problem.h:504-590
+  * parameters of "wave", "heat-rk", "heat-impl"   applications/wave/wave-app.cc:62-285
+
+The mass / system solves are exact (dense LU): the reference's CG with
+AMG / ILU to ReductionControl(1000, 1e-20, 1e-14) converges in 1-2 steps on
+these 41-DoF systems (the "[L] solved in N" lines), i.e. to the same values
+within 1e-14.  Pinned to applications/wave/tests/{wave_0,heat_0,heat_1}.output
+(tests/test_cut1d_golden.py); the level-set root is found by bisection to
+machine precision where deal.II's root finder stops at its tolerance, a
+difference far below the 9 printed digits.
+"""
+import math
+
+import numpy as np
+
+import oracle as O
+
+
+def gauss(n):
+    """QGauss(n) on [0, 1]."""
+    x, w = O.gauss(n)
+    return np.asarray(x), np.asarray(w)
+
+
+def gauss_lobatto(n):
+    """QGaussLobatto(n) on [0, 1] (FE_Q support points)."""
+    if n == 2:
+        return np.array([0.0, 1.0])
+    # interior points: roots of P'_{n-1}
+    c = np.zeros(n)
+    c[-1] = 1.0
+    r = np.polynomial.legendre.legroots(np.polynomial.legendre.legder(c))
+    return np.concatenate([[0.0], np.sort((r + 1.0) / 2.0), [1.0]])
+
+
+class DiscreteTime:
+    """deal.II DiscreteTime: fixed steps; the last one shrunk to hit end, or
+    the previous one stretched when the remainder is below 5 % of a step."""
+
+    def __init__(self, start, end, dt):
+        self.t, self.end, self.dt, self.step = start, end, dt, 0
+
+    def is_at_end(self):
+        return not (self.t < self.end)
+
+    def next_step_size(self):
+        if self.t + self.dt + 0.05 * self.dt > self.end:
+            return self.end - self.t
+        return self.dt
+
+    def advance(self):
+        h = self.next_step_size()
+        self.t = self.end if self.t + h >= self.end else self.t + h
+        self.step += 1
+
+
+RK4 = dict(a=[[], [0.5], [0.0, 0.5], [0.0, 0.0, 1.0]], b=[1 / 6, 1 / 3, 1 / 3, 1 / 6], c=[0.0, 0.5, 0.5, 1.0])
+
+
+def rk4_step(f, t, h, y):
+    """TimeStepping::ExplicitRungeKutta::evolve_one_time_step with
+    RK_CLASSIC_FOURTH_ORDER: k_i = f(t + c_i h, y + h sum_j a_ij k_j),
+    y += h sum_i b_i k_i."""
+    k = []
+    for i in range(4):
+        yi = y.copy()
+        for j, aij in enumerate(RK4["a"][i]):
+            if aij != 0.0:
+                yi = yi + h * aij * k[j]
+        k.append(f(t + RK4["c"][i] * h, yi))
+    for i in range(4):
+        y = y + h * RK4["b"][i] * k[i]
+    return y
+
+
+class Cut1D:
+    INSIDE, OUTSIDE, INTERSECTED = -1, 1, 0
+
+    def __init__(self, p, n_sub, left, right, level_set, ls_degree=None):
+        self.p, self.n = p, n_sub
+        self.left, self.right = left, right
+        self.h = (right - left) / n_sub
+        self.N = n_sub + 1
+        self.xv = np.array([left + i * self.h for i in range(self.N)])
+        self.level_set = level_set
+        k = ls_degree if ls_degree is not None else p
+        self.gl = gauss_lobatto(k + 1)
+        self.qx, self.qw = gauss(p + 1)
+        self._shape_cache = {}
+        self.cells = [self._cell(c) for c in range(n_sub)]
+
+    # -- GDM indexing (system.h:195-246, 404-424) --------------------------
+    def category(self, c):
+        p, n = self.p, self.n
+        return c if c < p // 2 else (p // 2 if c < n - p // 2 else p + c - n)
+
+    def offset(self, c):
+        p, n = self.p, self.n
+        return 0 if c < p // 2 else min(n, c + p // 2 + 1) - p
+
+    def _cell(self, c):
+        x0 = self.xv[c]
+        # FE_Q(k) interpolant of the level set on the cell (Lagrange through GL points)
+        vals = np.array([self.level_set(x0 + s * self.h) for s in self.gl])
+        if np.all(vals < 0):
+            loc = self.INSIDE
+        elif np.all(vals > 0):
+            loc = self.OUTSIDE
+        else:
+            loc = self.INTERSECTED
+
+        def phi(s):  # interpolant at reference coordinate s
+            r = 0.0
+            for a, sa in enumerate(self.gl):
+                la = 1.0
+                for b, sb in enumerate(self.gl):
+                    if b != a:
+                        la *= (s - sb) / (sa - sb)
+                r += vals[a] * la
+            return r
+
+        cell = dict(c=c, x0=x0, cat=self.category(c), off=self.offset(c), loc=loc, surface=[])
+        if loc == self.INSIDE:
+            cell["q"] = [(x0 + s * self.h, w * self.h) for s, w in zip(self.qx, self.qw)]
+        elif loc == self.OUTSIDE:
+            cell["q"] = []
+        else:
+            # roots of the interpolant in (0, 1): sign changes on a fine grid + bisection
+            grid = np.linspace(0.0, 1.0, 65)
+            pv = [phi(s) for s in grid]
+            roots = []
+            for a in range(64):
+                if pv[a] == 0.0:
+                    roots.append(grid[a])
+                elif pv[a] * pv[a + 1] < 0:
+                    lo, hi = grid[a], grid[a + 1]
+                    flo = pv[a]
+                    for _ in range(200):
+                        mid = 0.5 * (lo + hi)
+                        if mid == lo or mid == hi:
+                            break
+                        fm = phi(mid)
+                        if (fm < 0) == (flo < 0):
+                            lo, flo = mid, fm
+                        else:
+                            hi = mid
+                    roots.append(0.5 * (lo + hi))
+            pts = [0.0] + roots + [1.0]
+            q = []
+            for a, b in zip(pts[:-1], pts[1:]):
+                if phi(0.5 * (a + b)) < 0:  # inside sub-interval
+                    q += [(x0 + (a + (b - a) * s) * self.h, (b - a) * w * self.h) for s, w in zip(self.qx, self.qw)]
+            cell["q"] = q
+            for r in roots:
+                # level-set normal (gradient direction) at the root, finite difference of the interpolant
+                e = 1e-7
+                g = phi(min(r + e, 1.0)) - phi(max(r - e, 0.0))
+                cell["surface"].append((x0 + r * self.h, 1.0 if g > 0 else -1.0))
+        return cell
+
+    def shapes(self, cell, x, order):
+        """values (order 0) or x-derivatives (order 1) of the p+1 local shapes at x"""
+        key = (cell["c"], x, order)
+        v = self._shape_cache.get(key)
+        if v is None:
+            s = (x - cell["x0"]) / self.h
+            v = np.array([O.basis_value(self.p, cell["cat"], i, s, order) / self.h ** order
+                          for i in range(self.p + 1)])
+            self._shape_cache[key] = v
+        return v
+
+    def dofs(self, cell):
+        return cell["off"] + np.arange(self.p + 1)
+
+    # -- ghost-penalty faces (mass.h:86-105 / stiffness.h:80-98) ------------
+    def gp_faces(self):
+        """(cell, neighbour, face point) for every (cell, face) pair the
+        reference visits; each interior face near a cut is visited from both
+        sides (the 0.5 factors)."""
+        out = []
+        for c, cell in enumerate(self.cells):
+            if cell["loc"] == self.OUTSIDE:
+                continue
+            for f, nb in ((0, c - 1), (1, c + 1)):
+                if nb < 0 or nb >= self.n:
+                    continue
+                nl = self.cells[nb]["loc"]
+                if (cell["loc"] == self.INTERSECTED and nl != self.OUTSIDE) or \
+                        (nl == self.INTERSECTED and cell["loc"] != self.OUTSIDE):
+                    out.append((c, nb, self.xv[c + f]))
+        return out
+
+    def _jump_grad(self, c, nb, xf):
+        """global DoF -> [dphi/dx] = (from cell c) - (from neighbour) at face xf"""
+        key = ("jump", c, nb)
+        if key in self._shape_cache:
+            return self._shape_cache[key]
+        j = {}
+        for cc, sgn in ((c, 1.0), (nb, -1.0)):
+            cell = self.cells[cc]
+            g = self.shapes(cell, xf, 1)
+            for i, d in enumerate(self.dofs(cell)):
+                j[d] = j.get(d, 0.0) + sgn * g[i]
+        self._shape_cache[key] = j
+        return j
+
+    # -- matrices -----------------------------------------------------------
+    def mass_matrix(self, gamma_M):
+        M = np.zeros((self.N, self.N))
+        for cell in self.cells:
+            if cell["loc"] == self.OUTSIDE:
+                continue
+            d = self.dofs(cell)
+            for x, jxw in cell["q"]:
+                v = self.shapes(cell, x, 0)
+                M[np.ix_(d, d)] += np.outer(v, v) * jxw
+        for c, nb, xf in self.gp_faces():
+            j = self._jump_grad(c, nb, xf)
+            keys = list(j)
+            for a in keys:
+                for b in keys:
+                    M[a, b] += 0.5 * gamma_M * self.h ** 3 * j[a] * j[b]
+        for i in range(self.N):
+            if M[i, i] == 0.0:
+                M[i, i] = 1.0
+        return M
+
+    def stiffness_matrix(self, gamma_A, nitsche, with_surface=True):
+        S = np.zeros((self.N, self.N))
+        for cell in self.cells:
+            if cell["loc"] == self.OUTSIDE:
+                continue
+            d = self.dofs(cell)
+            for x, jxw in cell["q"]:
+                g = self.shapes(cell, x, 1)
+                S[np.ix_(d, d)] += np.outer(g, g) * jxw
+            if with_surface:
+                for xs, n in cell["surface"]:
+                    v, g = self.shapes(cell, xs, 0), self.shapes(cell, xs, 1)
+                    S[np.ix_(d, d)] += (-n * np.outer(g, v) - n * np.outer(v, g) +
+                                        nitsche / self.h * np.outer(v, v))
+        for c, nb, xf in self.gp_faces():
+            j = self._jump_grad(c, nb, xf)
+            for a in j:
+                for b in j:
+                    S[a, b] += 0.5 * gamma_A * self.h ** 3 * j[a] * j[b]
+        for i in range(self.N):
+            if S[i, i] == 0.0:
+                S[i, i] = 1.0
+        return S
+
+    def rhs(self, u, t, impl, gamma_A, nitsche, f=None, g=None):
+        """StiffnessMatrixOperator::compute_rhs (wave/stiffness.h:42-407),
+        location inside, no domain Dirichlet data"""
+        r = np.zeros(self.N)
+        for cell in self.cells:
+            if cell["loc"] == self.OUTSIDE:
+                continue
+            d = self.dofs(cell)
+            ul = u[d]
+            cv = np.zeros(self.p + 1)
+            for x, jxw in cell["q"]:
+                v, gr = self.shapes(cell, x, 0), self.shapes(cell, x, 1)
+                if impl:
+                    cv -= gr * (gr @ ul) * jxw
+                if f is not None:
+                    cv += f(x, t) * v * jxw
+            if g is not None:
+                for xs, n in cell["surface"]:
+                    v, gr = self.shapes(cell, xs, 0), self.shapes(cell, xs, 1)
+                    uq, duq = v @ ul, gr @ ul
+                    if impl:
+                        cv -= (-n * gr * uq - n * duq * v + nitsche / self.h * v * uq)
+                    cv += g(xs, t) * (nitsche / self.h * v - n * gr)
+            r[d] += cv
+        if impl:
+            for c, nb, xf in self.gp_faces():
+                j = self._jump_grad(c, nb, xf)
+                ju = sum(j[a] * u[a] for a in j)
+                for a in j:
+                    r[a] -= 0.5 * gamma_A * self.h * j[a] * ju
+        return r
+
+    def errors(self, u, exact, t):
+        """problem.h:504-590: (L2, L1, Linf) over the inside quadrature"""
+        l2, l1, linf = 0.0, 0.0, 0.0
+        for cell in self.cells:
+            if cell["loc"] == self.OUTSIDE:
+                continue
+            ul = u[self.dofs(cell)]
+            for x, jxw in cell["q"]:
+                e = self.shapes(cell, x, 0) @ ul - exact(x, t)
+                l2 += e * e * jxw
+                l1 += abs(e) * jxw
+                linf = max(linf, abs(e))
+        return math.sqrt(l2), l1, linf
+
+    def interpolate(self, fun, t):
+        """GDM::VectorTools::interpolate: vertex values (vector_tools.h:11-23)"""
+        return np.array([fun(x, t) for x in self.xv])
+
+
+# -- applications/wave/wave-app.cc parameter sets (dim = 1) -----------------
+def _sphere(x):
+    return abs(x) - 1.0
+
+
+def wave_params():
+    k = 1.5 * math.pi
+    ex = lambda x, t: math.cos(k * abs(x)) * math.cos(k * t)
+    return dict(p=3, n=40, left=-1.21, right=1.21, gamma_M=0.25 * math.sqrt(3.0), gamma_A=0.5 * math.sqrt(3.0),
+                nitsche=15.0, g=ex, f=None, exact=ex, start_t=0.0, end_t=2.0, cfl=0.3, cfl_pow=1.0)
+
+
+def heat_params(kind):
+    ex = lambda x, t: x ** 9 * math.exp(-t)
+    f = lambda x, t: -x ** 7 * math.exp(-t) * (x * x + 72)
+    cfl, cfl_pow = (0.3 / 9.0, 2.0) if kind == "heat-rk" else (0.3, 1.0)
+    return dict(p=3, n=40, left=-1.21, right=1.21, gamma_M=0.75, gamma_A=1.5, nitsche=15.0, g=ex, f=f, exact=ex,
+                start_t=0.0, end_t=0.1, cfl=cfl, cfl_pow=cfl_pow)
+
+
+def run(simulation, max_steps=None):
+    """Returns the postprocess table [(counter, t, L2, L1, Linf)] of
+    WaveProblem<1>::run for simulation in {"wave", "heat-rk", "heat-impl"}."""
+    P = wave_params() if simulation == "wave" else heat_params(simulation)
+    m = Cut1D(P["p"], P["n"], P["left"], P["right"], _sphere)
+    M = m.mass_matrix(P["gamma_M"])
+    Minv = np.linalg.inv(M)
+    dt = P["cfl"] * m.h ** P["cfl_pow"]
+    time = DiscreteTime(P["start_t"], P["end_t"], dt)
+    rows = []
+
+    def post(t, u, counter):
+        rows.append((counter, t) + m.errors(u, P["exact"], t))
+
+    u = m.interpolate(P["exact"], P["start_t"])
+    post(0.0, u, 0)
+    if simulation == "wave":
+        y = np.concatenate([u, np.zeros_like(u)])
+        N = m.N
+
+        def f(t, y):
+            r = m.rhs(y[:N], t, True, P["gamma_A"], P["nitsche"], f=P["f"], g=P["g"])
+            return np.concatenate([y[N:], Minv @ r])
+    elif simulation == "heat-rk":
+        y = u
+
+        def f(t, y):
+            return Minv @ m.rhs(y, t, True, P["gamma_A"], P["nitsche"], f=P["f"], g=P["g"])
+    else:
+        S = m.stiffness_matrix(P["gamma_A"], P["nitsche"])
+    n = 0
+    while not time.is_at_end() and (max_steps is None or n < max_steps):
+        t0, h = time.t, time.next_step_size()
+        if simulation == "heat-impl":
+            rhs = h * m.rhs(u, t0 + h, False, P["gamma_A"], P["nitsche"], f=P["f"], g=P["g"]) + M @ u
+            u = np.linalg.solve(M + h * S, rhs)
+        else:
+            y = rk4_step(f, t0, h, y)
+            u = y[:m.N]
+        n += 1
+        post(t0 + h, u, n)
+        time.advance()
+    return rows
