@@ -18,6 +18,7 @@
 #include "../../include/gdm_hip.h"
 #include "gdm_coeffs.h"
 #include "gdm_kernels.h"
+#include "gdm_rk.h"
 #include "gdm_setup.h"
 
 namespace {
@@ -114,6 +115,8 @@ struct gdm_op {
   double *cst3[3] = {nullptr, nullptr, nullptr};
   int row_lo3[3] = {0, 0, 0}, row_hi3[3] = {0, 0, 0};
   std::vector<double> cst3_host[3];
+  double *bc_tab = nullptr;  // gdm_eval_boundary: per-face 1D factor tables
+  int bc_tab_ld = 0;
   std::vector<Face> faces;
   double *face_tmp = nullptr;
   int64_t face_tmp_size = 0;
@@ -962,6 +965,67 @@ int gdm_vec_axpby(gdm_op *op, int64_t n, double a, const double *x, double b, do
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   hip_check(gdmk_launch_axpby(n, a, x, b, y, op->stream), "axpby");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_vec_rk_update(gdm_op *op, int64_t n, double beta, const double *k, const double *acc_in, double *acc_out,
+                      double alpha, const double *y, double *Y) {
+  if (!op || (n > 0 && (!k || !acc_in || !acc_out || (Y && !y)))) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  hip_check(gdmk_launch_rk_update(n, beta, k, acc_in, acc_out, alpha, y, Y, op->stream), "rk_update");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_params, double t, int derivative,
+                      double *bc_values) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_bc_points > 0 && !bc_values) return fail(GDM_ERR_ARG, "NULL bc_values");
+  const int need[3] = {1, 1 + op->dim, 9};
+  if (fn_kind < 0 || fn_kind > 2) return fail(GDM_ERR_ARG, "unknown gdm_fn_kind");
+  if (n_params < need[fn_kind] || (n_params > 0 && !params)) return fail(GDM_ERR_ARG, "too few function parameters");
+  if (op->faces.size() > 6 || op->p + 1 > 10) return fail(GDM_ERR_UNSUPPORTED, "boundary geometry");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  gdmk::BcGeom g{};
+  g.dim = op->dim;
+  g.p = op->p;
+  g.n_faces = (int)op->faces.size();
+  g.n_points = op->layout.n_bc_points;
+  for (int d = 0; d < 3; ++d) {
+    g.n_sub[d] = op->mesh.n_subdivisions[d];
+    g.lo[d] = op->mesh.lo[d];
+    g.hi[d] = op->mesh.hi[d];
+  }
+  for (int q = 0; q <= op->p; ++q) g.xq[q] = op->xq[q];
+  for (size_t f = 0; f < op->faces.size(); ++f) {
+    const Face &F = op->faces[f];
+    gdmk::BcFace &B = g.face[f];
+    B.offset = F.offset;
+    B.d = F.d;
+    B.side = F.side;
+    const FaceDir *T[2] = {&F.t0, &F.t1};
+    for (int k = 0; k < 2; ++k) {
+      B.Q[k] = T[k]->Q;
+      B.dim_index[k] = T[k]->dim_index;
+      B.cell_begin[k] = T[k]->cell_begin;
+    }
+  }
+  gdmk::BcFn fn{};
+  fn.kind = fn_kind;
+  fn.dim = op->dim;
+  for (int i = 0; i < n_params && i < 12; ++i) fn.prm[i] = params[i];
+  int ld = 1;
+  for (const Face &F : op->faces) ld = std::max({ld, F.t0.Q, F.t1.Q});
+  if (!op->bc_tab || op->bc_tab_ld < ld) {
+    std::vector<double> zero((size_t)6 * 3 * ld * 2, 0.0);
+    op->bc_tab = keep(op, dev_upload(zero));
+    op->bc_tab_ld = ld;
+  }
+  hip_check(gdmk_launch_bc_eval(g, fn, t, derivative ? 1 : 0, bc_values, op->bc_tab, op->bc_tab_ld, op->stream),
+            "bc_eval");
   return GDM_OK;
   GDM_GUARD_END
 }

@@ -1,0 +1,41 @@
+// gdm_rk.h -- device-side argument blocks and launchers of gdm_rk.hip
+// (device-resident RK stage updates and boundary-function evaluation).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gdmk {
+
+// Boundary-point geometry for device evaluation of boundary functions
+// (gdm_rk.hip): the device block(0) order, face by face, [q_t1][q_t0].
+struct BcFace {
+  int64_t offset;     // first point of the face in the bc array
+  int Q[2];           // points along t0, t1
+  int dim_index[2];   // reference directions of t0, t1 (-1 = trivial)
+  int cell_begin[2];  // first local cell along t0, t1
+  int d, side;        // normal direction, 0 = lo / 1 = hi
+};
+struct BcGeom {
+  int dim, p, n_faces;
+  int64_t n_points;
+  int n_sub[3];
+  double lo[3], hi[3];
+  double xq[10];  // QGauss(p+1) points on [0, 1]
+  BcFace face[6];
+};
+// built-in boundary functions (include/gdm_hip.h gdm_fn_kind)
+struct BcFn {
+  int kind, dim;
+  double prm[12];
+};
+
+}  // namespace gdmk
+
+extern "C" {
+// gdm_rk.hip: acc_out = acc_in + beta k; Y = y + alpha k (Y may be NULL)
+hipError_t gdmk_launch_rk_update(int64_t n, double beta, const double *k, const double *acc_in, double *acc_out,
+                                 double alpha, const double *y, double *Y, hipStream_t st);
+// tab: scratch of n_faces * 3 * ld * 2 doubles, ld >= max(Q0, Q1)
+hipError_t gdmk_launch_bc_eval(const gdmk::BcGeom &g, const gdmk::BcFn &f, double t, int derivative, double *out,
+                               double *tab, int ld, hipStream_t st);
+}

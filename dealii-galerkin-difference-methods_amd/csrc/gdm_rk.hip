@@ -1,0 +1,151 @@
+// gdm_rk.hip -- device-resident explicit Runge-Kutta stages.
+//
+// The reference evolves y = (block(0), block(1)) with
+// TimeStepping::ExplicitRungeKutta (applications/advection/include/gdm/
+// advection/problem.h:40-102, applications/wave/include/gdm/wave/problem.h:
+// 280-346): per stage a new BlockVector (problem.h:64-65), k_i = f(t + c_i h,
+// y + h sum_j a_ij k_j), then y += h sum_i b_i k_i, and block(0) (the boundary
+// values at the face quadrature points) is reset to g(t_n) every step by
+// initialize_time_step and evolved with dg/dt in the stages
+// (advection/stiffness.h:181-194, 286-289).
+//
+// Here the RK state never leaves HBM:
+//   * rk_update: acc_out = acc_in + beta k and (optionally) Y = y + alpha k in
+//     one pass -- the low-storage form of a Butcher table with one nonzero
+//     a_ij per stage (classic RK4): the b-sum is accumulated as the stages
+//     are produced, in the same order as deal.II's final sadd loop;
+//   * boundary functions: g(t) and dg/dt(t) of built-in analytic functions
+//     evaluated at the boundary points straight from the face geometry
+//     (coordinates computed from the point index, no coordinate array), so
+//     no host evaluation and no H2D copy happen inside the RK loop.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "gdm_kernels.h"
+#include "gdm_rk.h"
+
+namespace gdmk {
+
+__global__ void __launch_bounds__(256) rk_update_kernel(int64_t n, double beta, const double *__restrict__ k,
+                                                        const double *acc_in, double *acc_out, double alpha,
+                                                        const double *__restrict__ y, double *__restrict__ Y) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (Y) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const double ki = k[i];
+      acc_out[i] = acc_in[i] + beta * ki;
+      Y[i] = y[i] + alpha * ki;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+      acc_out[i] = acc_in[i] + beta * k[i];
+  }
+}
+
+namespace {
+
+// coordinate of quadrature point qi along face direction slot k (0 = t0, 1 = t1)
+__device__ __forceinline__ double slot_coord(const BcFace &F, const BcGeom &g, int k, int qi) {
+  const int e = F.dim_index[k];
+  const int n1 = g.p + 1;
+  const int c = F.cell_begin[k] + qi / n1, qq = qi - (qi / n1) * n1;
+  const double h = (g.hi[e] - g.lo[e]) / g.n_sub[e];
+  return g.lo[e] + (c + g.xq[qq]) * h;
+}
+
+// separable factor of GDM_FN_SINE_PRODUCT in direction e at coordinate x:
+// (s, c) = (sin, cos) of 2 pi k_e (x - a_e t) + phi_e
+__device__ __forceinline__ void sine_factor(const BcFn &f, int e, double x, double t, double &s, double &c) {
+  const double arg = 2.0 * M_PI * f.prm[3 + e] * (x - f.prm[e] * t) + f.prm[6 + e];
+  sincos(arg, &s, &c);
+}
+
+}  // namespace
+
+// Separable functions: per face, the 1D factors along t0 / t1 / the normal
+// are tabulated once (tab[slot][q] = (s, c); slot 2 = the normal coordinate),
+// so a boundary point costs two table reads and a few multiplies instead of
+// 2 * dim transcendental evaluations.
+__global__ void __launch_bounds__(256) bc_table_kernel(BcGeom g, BcFace F, BcFn f, double t, double *tab, int ld) {
+  const int slot = blockIdx.y;  // 0: t0, 1: t1, 2: normal
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < (slot < 2 ? F.Q[slot] : 1); q += gridDim.x * blockDim.x) {
+    double s = 1.0, c = 0.0;
+    if (slot < 2 && F.dim_index[slot] >= 0)
+      sine_factor(f, F.dim_index[slot], slot_coord(F, g, slot, q), t, s, c);
+    else if (slot == 2)
+      sine_factor(f, F.d, F.side ? g.hi[F.d] : g.lo[F.d], t, s, c);
+    tab[((size_t)slot * ld + q) * 2] = s;
+    tab[((size_t)slot * ld + q) * 2 + 1] = c;
+  }
+}
+
+// one face: grid (ceil(Q0 / 256), Q1); i1 = blockIdx.y, i0 = lane index
+__global__ void __launch_bounds__(256) bc_face_kernel(BcGeom g, BcFace F, BcFn f, double t, int derivative,
+                                                      const double *__restrict__ tab, int ld, double *out) {
+  const int i1 = blockIdx.y;
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 >= F.Q[0]) return;
+  double *o = out + F.offset + (int64_t)i1 * F.Q[0] + i0;
+  if (f.kind == 0) {
+    *o = derivative ? 0.0 : f.prm[0];
+    return;
+  }
+  if (f.kind == 1) {  // cone max(0, r0 - |x - c|) (applications/advection/advection-app.cc:51-79), dg/dt = 0
+    if (derivative) {
+      *o = 0.0;
+      return;
+    }
+    double x[3] = {0.0, 0.0, 0.0};
+    x[F.d] = F.side ? g.hi[F.d] : g.lo[F.d];
+    if (F.dim_index[0] >= 0) x[F.dim_index[0]] = slot_coord(F, g, 0, i0);
+    if (F.dim_index[1] >= 0) x[F.dim_index[1]] = slot_coord(F, g, 1, i1);
+    double r2 = 0.0;
+    for (int d = 0; d < g.dim; ++d) r2 += (x[d] - f.prm[1 + d]) * (x[d] - f.prm[1 + d]);
+    *o = fmax(0.0, f.prm[0] - sqrt(r2));
+    return;
+  }
+  // kind 2: prod_d sin(.) over the dim directions; trivial slots hold (1, 0)
+  const double s0 = tab[2 * i0], c0 = tab[2 * i0 + 1];
+  const double s1 = tab[2 * ((size_t)ld + i1)], c1 = tab[2 * ((size_t)ld + i1) + 1];
+  const double sn = tab[2 * (size_t)2 * ld], cn = tab[2 * (size_t)2 * ld + 1];
+  if (!derivative) {
+    *o = s0 * s1 * sn;
+    return;
+  }
+  // d/dt: sum over directions of -2 pi k_e a_e cos(.) * the other sines
+  double r = 0.0;
+  if (F.dim_index[0] >= 0) r += -2.0 * M_PI * f.prm[3 + F.dim_index[0]] * f.prm[F.dim_index[0]] * c0 * s1 * sn;
+  if (F.dim_index[1] >= 0) r += -2.0 * M_PI * f.prm[3 + F.dim_index[1]] * f.prm[F.dim_index[1]] * s0 * c1 * sn;
+  r += -2.0 * M_PI * f.prm[3 + F.d] * f.prm[F.d] * s0 * s1 * cn;
+  *o = r;
+}
+
+}  // namespace gdmk
+
+extern "C" hipError_t gdmk_launch_rk_update(int64_t n, double beta, const double *k, const double *acc_in,
+                                           double *acc_out, double alpha, const double *y, double *Y,
+                                           hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(gdmk::rk_update_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n, beta, k, acc_in, acc_out,
+                     alpha, y, Y);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gdmk_launch_bc_eval(const gdmk::BcGeom &g, const gdmk::BcFn &f, double t, int derivative,
+                                         double *out, double *tab, int ld, hipStream_t st) {
+  for (int fi = 0; fi < g.n_faces; ++fi) {
+    const gdmk::BcFace &F = g.face[fi];
+    if ((int64_t)F.Q[0] * F.Q[1] <= 0) continue;
+    if (f.kind == 2) {
+      hipLaunchKernelGGL(gdmk::bc_table_kernel, dim3((unsigned)((ld + 255) / 256), 3), dim3(256), 0, st, g, F, f, t,
+                         tab + (size_t)fi * 3 * ld * 2, ld);
+    }
+    hipLaunchKernelGGL(gdmk::bc_face_kernel, dim3((unsigned)((F.Q[0] + 255) / 256), (unsigned)F.Q[1]), dim3(256), 0,
+                       st, g, F, f, t, derivative, tab + (size_t)fi * 3 * ld * 2, ld, out);
+  }
+  return hipGetLastError();
+}

@@ -85,6 +85,8 @@ def load():
         "gdm_mass_solve_lines": [P, i32, P, i64, i64, i64, i64, i64],
         "gdm_vec_axpby": [P, i64, d, P, d, P],
         "gdm_vec_dot": [P, i64, P, P, ctypes.POINTER(d)],
+        "gdm_vec_rk_update": [P, i64, d, P, P, P, d, P, P],
+        "gdm_eval_boundary": [P, i32, P, i32, d, i32, P],
         "gdm_synchronize": [P],
         "gdm_malloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
         "gdm_free": [P, P],

@@ -156,6 +156,27 @@ class GdmOperator:
         check(self.lib.gdm_vec_axpby(self.h, x.numel(), float(a), _ptr(x), float(b), _ptr(y)), "gdm_vec_axpby")
         return y
 
+    def rk_update(self, beta, k, acc_in, acc_out, alpha=0.0, y=None, Y=None):
+        """acc_out = acc_in + beta k; Y = y + alpha k (when Y is given), one pass"""
+        n = k.numel()
+        for v in (acc_in, acc_out) + ((y, Y) if Y is not None else ()):
+            if v.numel() != n:
+                raise GdmError("rk_update: vector sizes differ")
+        check(self.lib.gdm_vec_rk_update(self.h, n, float(beta), _ptr(k), _ptr(acc_in), _ptr(acc_out), float(alpha),
+                                         _ptr(y) if Y is not None else None, _ptr(Y)), "gdm_vec_rk_update")
+        return acc_out
+
+    FN_CONSTANT, FN_CONE, FN_SINE_PRODUCT = 0, 1, 2
+
+    def eval_boundary(self, fn_kind, params, t, derivative, out):
+        """out (device order, n_bc_points) = g(t) or dg/dt(t) of a built-in function"""
+        if out.numel() != self.n_bc_points:
+            raise GdmError("eval_boundary: out has %d entries, expected %d" % (out.numel(), self.n_bc_points))
+        prm = (ctypes.c_double * max(len(params), 1))(*[float(v) for v in params])
+        check(self.lib.gdm_eval_boundary(self.h, int(fn_kind), prm, len(params), float(t), int(derivative),
+                                         _ptr(out)), "gdm_eval_boundary")
+        return out
+
     def dot(self, x, y):
         r = ctypes.c_double(0.0)
         check(self.lib.gdm_vec_dot(self.h, x.numel(), _ptr(x), _ptr(y), ctypes.byref(r)), "gdm_vec_dot")

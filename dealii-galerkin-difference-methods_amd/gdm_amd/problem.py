@@ -1,0 +1,157 @@
+"""Device-resident time integration: the RK drivers of the reference's
+problems over the C ABI, every vector in HBM.
+
+  AdvectionProblem   applications/advection/include/gdm/advection/problem.h:31-102
+                     (non-composite branch): y = (block(0) boundary values,
+                     block(1) u); f(t, y) = (dg/dt, M^-1 (K u + inflow data))
+  WaveProblem        applications/wave/include/gdm/wave/problem.h:280-346
+                     (wave-rk): y = (u, v); f(t, y) = (v, M^-1 K u)
+
+Both use TimeStepping::ExplicitRungeKutta with RK_CLASSIC_FOURTH_ORDER and
+DiscreteTime, restated in low-storage form: the b-weighted sum of the stages
+is accumulated as each stage is produced (gdm_vec_rk_update: one pass writes
+the accumulator and the next stage vector), in the same order as deal.II's
+final y.sadd loop, so no per-stage BlockVector is allocated (problem.h:64-65)
+and nothing crosses PCIe inside the loop.  Block(0) of the advection problem
+is g(t_n) at the start of every step (initialize_time_step,
+advection/stiffness.h:181-194) and dg/dt at the stage times
+(stiffness.h:286-289), both evaluated on the device for the built-in
+boundary functions (gdm_eval_boundary).
+"""
+from ._capi import GdmError
+
+# RK_CLASSIC_FOURTH_ORDER (deal.II TimeStepping): c, a_{i,i-1}, b
+RK4_C = (0.0, 0.5, 0.5, 1.0)
+RK4_A = (0.5, 0.5, 1.0)
+RK4_B = (1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0)
+
+
+class DiscreteTime:
+    """deal.II DiscreteTime: fixed steps; the last one shrunk to hit the end
+    time, or the previous one stretched when the remainder is below 5 %."""
+
+    def __init__(self, start, end, dt):
+        self.t, self.end, self.dt, self.step = float(start), float(end), float(dt), 0
+
+    def is_at_end(self):
+        return not (self.t < self.end)
+
+    def next_step_size(self):
+        if self.t + self.dt + 0.05 * self.dt > self.end:
+            return self.end - self.t
+        return self.dt
+
+    def advance(self):
+        h = self.next_step_size()
+        self.t = self.end if self.t + h >= self.end else self.t + h
+        self.step += 1
+
+
+class WaveProblem:
+    """wave-rk on one rank: du/dt = v, dv/dt = M^-1 (K u) with K the wave
+    operator of `op` (kind "wave": -(grad v, grad u) [+ box Nitsche])."""
+
+    def __init__(self, op):
+        if op.mesh.n_ranks != 1:
+            raise GdmError("WaveProblem: single-rank driver (multi-rank: gdm_amd.distributed)")
+        self.op = op
+        n = op.n_owned
+        self.u, self.v = op.new_vector(False), op.new_vector(False)
+        self._acc = [op.new_vector(False) for _ in range(2)]
+        self._Y = [op.new_vector(False) for _ in range(2)]
+        self._kv = op.new_vector(False)
+        self.n = n
+
+    def rhs(self, t, U, out):
+        """dv/dt = M^-1 compute_rhs(U) (wave/problem.h:313-317)"""
+        self.op.apply(U, out)
+        self.op.mass_solve(out, out)
+        return out
+
+    def step(self, t, h):
+        op, y = self.op, (self.u, self.v)
+        acc, Y, kv = self._acc, self._Y, self._kv
+        stage = y
+        for s in range(4):
+            # k = (stage_v, M^-1 K stage_u)
+            self.rhs(t + RK4_C[s] * h, stage[0], kv)
+            ku = stage[1]
+            last = s == 3
+            acc_in = y if s == 0 else acc
+            acc_out = y if last else acc
+            a_next = 0.0 if last else h * RK4_A[s]
+            # u block first: it reads ku = stage_v before the v block overwrites Y_v
+            op.rk_update(h * RK4_B[s], ku, acc_in[0], acc_out[0], a_next, None if last else y[0],
+                         None if last else Y[0])
+            op.rk_update(h * RK4_B[s], kv, acc_in[1], acc_out[1], a_next, None if last else y[1],
+                         None if last else Y[1])
+            stage = Y
+
+    def run(self, start_t, end_t, dt, max_steps=None, callback=None):
+        time = DiscreteTime(start_t, end_t, dt)
+        n = 0
+        while not time.is_at_end() and (max_steps is None or n < max_steps):
+            h = time.next_step_size()
+            self.step(time.t, h)
+            n += 1
+            if callback is not None:
+                callback(time.t + h, self)
+            time.advance()
+        return n
+
+
+class AdvectionProblem:
+    """advection problem.h:31-102 on one rank with a built-in boundary
+    function (gdm_fn_kind) for g and dg/dt."""
+
+    def __init__(self, op, fn_kind, fn_params):
+        if op.mesh.n_ranks != 1:
+            raise GdmError("AdvectionProblem: single-rank driver")
+        self.op, self.fn, self.prm = op, int(fn_kind), list(fn_params)
+        nb = max(op.n_bc_points, 1)
+        import torch
+
+        dev = "cuda:%d" % op.device
+        z = lambda m: torch.zeros(m, dtype=torch.float64, device=dev)  # noqa: E731
+        self.u = op.new_vector(False)
+        self.bc = z(nb)
+        self._acc = [z(nb), op.new_vector(False)]
+        self._Y = [z(nb), op.new_vector(False)]
+        self._k = [z(nb), op.new_vector(False)]
+
+    def initialize_time_step(self, t):
+        """block(0) = g(t_n) at the boundary points (stiffness.h:181-194)"""
+        if self.op.n_bc_points:
+            self.op.eval_boundary(self.fn, self.prm, t, 0, self.bc)
+
+    def rhs(self, t, BC, U, kbc, ku):
+        op = self.op
+        if op.n_bc_points:
+            op.eval_boundary(self.fn, self.prm, t, 1, kbc)  # block(0) = dg/dt (stiffness.h:286-289)
+        op.apply(U, ku, BC if op.n_bc_points else None)
+        op.mass_solve(ku, ku)
+
+    def step(self, t, h):
+        op = self.op
+        self.initialize_time_step(t)
+        y = (self.bc, self.u)
+        acc, Y, k = self._acc, self._Y, self._k
+        stage = y
+        blocks = (0, 1) if op.n_bc_points else (1,)
+        for s in range(4):
+            self.rhs(t + RK4_C[s] * h, stage[0], stage[1], k[0], k[1])
+            last = s == 3
+            a_next = 0.0 if last else h * RK4_A[s]
+            for b in blocks:
+                op.rk_update(h * RK4_B[s], k[b], (y if s == 0 else acc)[b], (y if last else acc)[b], a_next,
+                             None if last else y[b], None if last else Y[b])
+            stage = Y
+
+    def run(self, start_t, end_t, dt, max_steps=None):
+        time = DiscreteTime(start_t, end_t, dt)
+        n = 0
+        while not time.is_at_end() and (max_steps is None or n < max_steps):
+            self.step(time.t, time.next_step_size())
+            n += 1
+            time.advance()
+        return n

@@ -3,13 +3,15 @@
 // (gdm/hip/operators.h), in the shape of
 // applications/advection/advection-app.cc:86-154 + problem.h:31-102.
 //
-//   advection_app DIM P N STEPS CFL OUT [DEVICE]
+//   advection_app DIM P N STEPS CFL OUT [DEVICE] [DEVBC]
 //
 // Manufactured solution u(x, t) = prod_d sin(2 pi (x_d - a_d t) + 0.3 d) on
 // [0, 1]^dim with a = (1, 0.15, -0.05) (prototypes/advection_01_gdm.cc:37-41);
 // inflow data and block(0) evolution from u and du/dt.  Writes the owned DoF
 // values after STEPS RK4 steps to OUT (raw little-endian doubles, reference
-// global order) and prints one line per step with |u|_2.
+// global order) and prints one line per step with |u|_2.  DEVBC = 1 evaluates
+// g and dg/dt on the device (GDM_FN_SINE_PRODUCT with the same parameters)
+// instead of the host callbacks.
 #include <gdm/hip/operators.h>
 
 #include <cstdio>
@@ -41,7 +43,7 @@ double dg_dt(const GDM::HIP::Point &x, double t) {
 }
 
 template <int dim>
-int run(int p, int n, int steps, double cfl, const char *out, int device) {
+int run(int p, int n, int steps, double cfl, const char *out, int device, int devbc) {
   GDM::HIP::Parameters<dim> params;
   params.fe_degree = p;
   params.n_subdivisions_1D = n;
@@ -55,6 +57,10 @@ int run(int p, int n, int steps, double cfl, const char *out, int device) {
   params.max_val = 1.0;
   for (int d = 0; d < dim; ++d) params.advection[d] = kA[d];
   params.device = device;
+  if (devbc) {
+    params.boundary_function = GDM_FN_SINE_PRODUCT;
+    params.boundary_function_params = {kA[0], kA[1], kA[2], 1.0, 1.0, 1.0, 0.0, 0.3, 0.6};
+  }
   GDM::HIP::AdvectionProblem<dim> problem(params);
   const unsigned int done = problem.run(steps);
   const std::vector<double> u = problem.get_solution();
@@ -76,11 +82,12 @@ int main(int argc, char **argv) {
   const int dim = std::atoi(argv[1]), p = std::atoi(argv[2]), n = std::atoi(argv[3]), steps = std::atoi(argv[4]);
   const double cfl = std::atof(argv[5]);
   const int device = argc > 7 ? std::atoi(argv[7]) : 0;
+  const int devbc = argc > 8 ? std::atoi(argv[8]) : 0;
   try {
     switch (dim) {
-      case 1: return run<1>(p, n, steps, cfl, argv[6], device);
-      case 2: return run<2>(p, n, steps, cfl, argv[6], device);
-      case 3: return run<3>(p, n, steps, cfl, argv[6], device);
+      case 1: return run<1>(p, n, steps, cfl, argv[6], device, devbc);
+      case 2: return run<2>(p, n, steps, cfl, argv[6], device, devbc);
+      case 3: return run<3>(p, n, steps, cfl, argv[6], device, devbc);
       default: std::fprintf(stderr, "dim must be 1, 2 or 3\n"); return 2;
     }
   } catch (const GDM::HIP::Error &e) {

@@ -62,6 +62,13 @@ struct Parameters {
   std::array<double, dim> advection{};  // constant field a
   int device = 0;
   int n_ranks = 1, rank = 0;            // z-slab partition (system.h:720-757)
+  // Device evaluation of g / dg/dt at the boundary points (gdm_eval_boundary):
+  // a gdm_fn_kind (GDM_FN_CONE = the advection app's ExactSolution,
+  // advection-app.cc:51-79; GDM_FN_SINE_PRODUCT = a transported product of
+  // sines) and its parameters.  -1: evaluate the host callbacks above and
+  // upload (the reference's behaviour, a PCIe copy per stage).
+  int boundary_function = -1;
+  std::vector<double> boundary_function_params;
 };
 
 // A device buffer of doubles allocated through the engine (gdm_malloc).
@@ -107,6 +114,16 @@ class DeviceVector {
     if (x.n_ != n_) throw Error("DeviceVector::sadd: size mismatch");
     if (n_) check(gdm_vec_axpby(op_, (int64_t)n_, a, x.ptr_, b, ptr_), "gdm_vec_axpby");
   }
+  // this = acc_in + beta k and, when Y != nullptr, *Y = y + alpha k (one pass, gdm_vec_rk_update)
+  void rk_update(double beta, const DeviceVector &k, const DeviceVector &acc_in, double alpha = 0.0,
+                 const DeviceVector *y = nullptr, DeviceVector *Y = nullptr) {
+    if (k.n_ != n_ || acc_in.n_ != n_ || (Y && (Y->n_ != n_ || !y || y->n_ != n_)))
+      throw Error("DeviceVector::rk_update: size mismatch");
+    if (n_)
+      check(gdm_vec_rk_update(op_, (int64_t)n_, beta, k.ptr_, acc_in.ptr_, ptr_, alpha, Y ? y->ptr_ : nullptr,
+                              Y ? Y->ptr_ : nullptr),
+            "gdm_vec_rk_update");
+  }
   double operator*(const DeviceVector &x) const {
     double r = 0.0;
     check(gdm_vec_dot(op_, (int64_t)n_, ptr_, x.ptr_, &r), "gdm_vec_dot");
@@ -139,6 +156,24 @@ struct BlockVector {
     b1.sadd(b, a, x.b1);
   }
 };
+
+// RK_CLASSIC_FOURTH_ORDER (deal.II TimeStepping): c_i, a_{i,i-1}, b_i
+struct ClassicRK4 {
+  static constexpr double c[4] = {0.0, 0.5, 0.5, 1.0};
+  static constexpr double a[4] = {0.0, 0.5, 0.5, 1.0};  // a[s] = a_{s,s-1}
+  static constexpr double b[4] = {1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0};
+};
+
+// One RK stage update in low-storage form (the b-sum accumulated as the stages
+// are produced, in the order of deal.II's final sadd loop): acc = (s == 0 ? y
+// : acc) + h b_s k; Y = y + h a_{s+1} k; the last stage writes y itself.
+inline void rk4_stage_update(int s, double h, const DeviceVector &k, DeviceVector &y, DeviceVector &acc,
+                             DeviceVector &Y) {
+  if (s == 3)
+    y.rk_update(h * ClassicRK4::b[3], k, acc);
+  else
+    acc.rk_update(h * ClassicRK4::b[s], k, s == 0 ? y : acc, h * ClassicRK4::a[s + 1], &y, &Y);
+}
 
 // .../advection/discretization.h: the mesh, categories and partition (held by
 // the engine) plus the quantities the problem driver reads.
@@ -186,6 +221,8 @@ class StiffnessMatrixOperator {
     check(gdm_op_set_stream(op, nullptr), "gdm_op_set_stream");
     exact_solution = params.exact_solution;
     exact_solution_der = params.exact_solution_der;
+    bc_fn = params.boundary_function;
+    bc_fn_params = params.boundary_function_params;
     // boundary points of the owned cells (device order), collect_boundary_points (:40-160)
     std::vector<double> xyz(3 * std::max<int64_t>(layout.n_bc_points, 1));
     check(gdm_bc_points(op, xyz.data()), "gdm_bc_points");
@@ -199,14 +236,14 @@ class StiffnessMatrixOperator {
   }
 
   void initialize_time_step(BlockVector &stage_bc_and_solution, const double time) const {
-    stage_bc_and_solution.block(0).upload(evaluate(exact_solution, time));
+    set_boundary(stage_bc_and_solution.block(0), time, 0);
   }
 
   // vec_rhs.block(1) (owned entries of its local layout) = K u + inflow
   // data; vec_rhs.block(0) = dg/dt at the boundary points.  The ghost planes of
   // src.block(1) must be current (update_ghost_values, stiffness.h:343).
   void compute_rhs(BlockVector &vec_rhs, const BlockVector &stage_bc_and_solution, const double time) const {
-    vec_rhs.block(0).upload(evaluate(exact_solution_der, time));
+    set_boundary(vec_rhs.block(0), time, 1);
     check(gdm_apply(op, stage_bc_and_solution.block(1).get_values(), owned(vec_rhs.block(1)),
                     stage_bc_and_solution.block(0).get_values()),
           "gdm_apply");
@@ -225,6 +262,19 @@ class StiffnessMatrixOperator {
     for (std::size_t i = 0; i < v.size(); ++i) v[i] = f ? f(all_points_0[i], t) : 0.0;
     return v;
   }
+  // block(0) <- g(t) (derivative 0) or dg/dt(t) (1): on the device for a
+  // built-in function, else host callbacks + upload
+  void set_boundary(DeviceVector &b0, double t, int derivative) const {
+    if (layout.n_bc_points == 0) return;
+    if (bc_fn >= 0)
+      check(gdm_eval_boundary(op, bc_fn, bc_fn_params.data(), (int)bc_fn_params.size(), t, derivative,
+                              b0.get_values()),
+            "gdm_eval_boundary");
+    else
+      b0.upload(evaluate(derivative ? exact_solution_der : exact_solution, t));
+  }
+  int bc_fn = -1;
+  std::vector<double> bc_fn_params;
   const Discretization<dim> &discretization;
   gdm_op *op = nullptr;
   gdm_layout layout{};
@@ -253,6 +303,26 @@ class MassMatrixOperator {
   void vmult(double *dst_owned, const double *src_local) const { check(gdm_mass_apply(op, src_local, dst_owned), "gdm_mass_apply"); }
   // x = M^-1 rhs (owned vectors)
   void solve(double *x_owned, const double *rhs_owned) const { check(gdm_mass_solve(op, rhs_owned, x_owned), "gdm_mass_solve"); }
+
+  // MassMatrixOperator::get_sparse_matrix (advection/mass.h:30-36): an object
+  // modelling deal.II's MatrixType -- vmult / Tvmult (M is symmetric) and
+  // m() / n() -- over the matrix-free mass; SolverCG and the solve() call
+  // sites take it where the reference takes the Trilinos matrix.
+  class SparseMatrix {
+   public:
+    explicit SparseMatrix(const MassMatrixOperator &M) : M(M) {}
+    // dst (owned entries) = M src (local layout, ghost planes current)
+    void vmult(DeviceVector &dst, const DeviceVector &src) const {
+      M.vmult(dst.get_values() + M.layout.ghost_planes_below * M.layout.plane_size, src.get_values());
+    }
+    void Tvmult(DeviceVector &dst, const DeviceVector &src) const { vmult(dst, src); }
+    std::size_t m() const { return (std::size_t)M.layout.n_dofs_global; }
+    std::size_t n() const { return (std::size_t)M.layout.n_dofs_global; }
+
+   private:
+    const MassMatrixOperator &M;
+  };
+  SparseMatrix get_sparse_matrix() const { return SparseMatrix(*this); }
   gdm_op *handle() const { return op; }
 
  private:
@@ -303,8 +373,12 @@ class AdvectionProblem {
     const double delta_t = discretization.get_dx() * params.cfl / params.max_val;  // problem.h:45
     stiffness_matrix_operator.initialize_dof_vector(solution);
     set_initial_condition(solution.block(1));
-    BlockVector k[4], stage;
-    for (auto &v : k) stiffness_matrix_operator.initialize_dof_vector(v);
+    // device-resident low-storage RK4: k (stage derivative), acc (b-sum), Y
+    // (next stage) -- no per-stage allocation (problem.h:64-65) and, with a
+    // device boundary function, no host evaluation or upload in the loop
+    BlockVector k, acc, stage;
+    stiffness_matrix_operator.initialize_dof_vector(k);
+    stiffness_matrix_operator.initialize_dof_vector(acc);
     stiffness_matrix_operator.initialize_dof_vector(stage);
     const auto fu_rhs = [&](double time, const BlockVector &y, BlockVector &result) {
       stiffness_matrix_operator.compute_rhs(result, y, time);
@@ -312,19 +386,15 @@ class AdvectionProblem {
       mass_matrix_operator.solve(r, r);
     };
     DiscreteTime time(params.start_t, params.end_t, delta_t);
-    static const double c[4] = {0.0, 0.5, 0.5, 1.0}, aa[4] = {0.0, 0.5, 0.5, 1.0},
-                        b[4] = {1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0};
     unsigned int n = 0;
     while (!time.is_at_end() && n < max_steps) {
       stiffness_matrix_operator.initialize_time_step(solution, time.get_current_time());  // evaluate bc
       const double t0 = time.get_current_time(), h = time.get_next_step_size();
       for (int s = 0; s < 4; ++s) {
-        // Y_s = y + h a_s k_{s-1}
-        stage.sadd(0.0, 1.0, solution);
-        if (s > 0) stage.sadd(1.0, h * aa[s], k[s - 1]);
-        fu_rhs(t0 + c[s] * h, s == 0 ? solution : stage, k[s]);
+        fu_rhs(t0 + ClassicRK4::c[s] * h, s == 0 ? solution : stage, k);
+        for (unsigned int bl = 0; bl < 2; ++bl)
+          rk4_stage_update(s, h, k.block(bl), solution.block(bl), acc.block(bl), stage.block(bl));
       }
-      for (int s = 0; s < 4; ++s) solution.sadd(1.0, h * b[s], k[s]);
       time.advance_time();
       ++n;
     }

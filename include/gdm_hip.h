@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 3
+#define GDM_HIP_ABI_VERSION 4
 
 enum gdm_status {
   GDM_OK = 0,
@@ -165,6 +165,35 @@ int gdm_mass_solve_lines(gdm_op *op, int axis, double *v, int64_t n_lines, int64
 int gdm_vec_axpby(gdm_op *op, int64_t n, double a, const double *x, double b, double *y);
 int gdm_vec_dot(gdm_op *op, int64_t n, const double *x, const double *y, double *result_host);
 int gdm_synchronize(gdm_op *op);
+
+/* ------------------------------------------------------------------------
+ * Device-resident explicit Runge-Kutta: replaces the per-stage
+ * BlockVector allocation and vector updates of TimeStepping::
+ * ExplicitRungeKutta (advection/problem.h:62-94, wave/problem.h:296-338) and
+ * the host evaluation of block(0) in initialize_time_step / compute_rhs
+ * (advection/stiffness.h:181-194, 286-289).
+ *
+ *   gdm_vec_rk_update   acc_out = acc_in + beta k and, when Y != NULL,
+ *                       Y = y + alpha k, in one pass (low-storage form of a
+ *                       Butcher table with one nonzero a_ij per stage, e.g.
+ *                       RK_CLASSIC_FOURTH_ORDER; acc_in may equal acc_out)
+ *   gdm_eval_boundary   bc_values (device order, n_bc_points) = g(t)
+ *                       (derivative 0) or dg/dt(t) (derivative 1) at the
+ *                       boundary points for a built-in function:
+ *     GDM_FN_CONSTANT      params: c
+ *     GDM_FN_CONE          params: r0, center[dim] -- max(0, r0 - |x - c|)
+ *                          (the advection app's ExactSolution,
+ *                          applications/advection/advection-app.cc:51-79;
+ *                          dg/dt = 0, its ExactSolutionDerivative)
+ *     GDM_FN_SINE_PRODUCT  params: a[3], k[3], phi[3] --
+ *                          prod_d sin(2 pi k_d (x_d - a_d t) + phi_d)
+ *                          (a solution transported with velocity a)
+ * ---------------------------------------------------------------------- */
+enum gdm_fn_kind { GDM_FN_CONSTANT = 0, GDM_FN_CONE = 1, GDM_FN_SINE_PRODUCT = 2 };
+int gdm_vec_rk_update(gdm_op *op, int64_t n, double beta, const double *k, const double *acc_in, double *acc_out,
+                      double alpha, const double *y, double *Y);
+int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_params, double t, int derivative,
+                      double *bc_values);
 
 /* memory helpers for callers without their own device allocator */
 int gdm_malloc(gdm_op *op, size_t bytes, void **ptr);

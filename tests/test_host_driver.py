@@ -82,12 +82,62 @@ def test_driver_fails_loudly_without_gpu(tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dim,p,n,steps", [(1, 3, 40, 4), (2, 5, 24, 3), (3, 3, 10, 2), (3, 5, 12, 2)])
-def test_driver_rk4_matches_oracle(tmp_path, dim, p, n, steps):
+@pytest.mark.parametrize("devbc", [0, 1])
+def test_driver_rk4_matches_oracle(tmp_path, dim, p, n, steps, devbc):
+    """devbc = 1: block(0) = g / dg/dt evaluated on the device (gdm_eval_boundary)"""
     out = tmp_path / "u.bin"
-    r = subprocess.run([APP, str(dim), str(p), str(n), str(steps), "0.1", str(out)], capture_output=True, text=True,
-                       timeout=120)
+    r = subprocess.run([APP, str(dim), str(p), str(n), str(steps), "0.1", str(out), "0", str(devbc)],
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     u = np.fromfile(out, dtype=np.float64)
     ref = oracle_rk4(dim, p, n, steps, 0.1)
     assert u.shape == ref.shape
     assert np.linalg.norm(u - ref) / np.linalg.norm(ref) < 1e-10
+
+
+WAVE_APP = os.path.join(ROOT, "dealii-galerkin-difference-methods_amd", "lib", "host", "wave_app")
+
+
+def wave_oracle(dim, p, n, steps, cfl, nitsche):
+    """wave/problem.h:280-346 (wave-rk) on the oracle's cell loop + exact mass
+    inverse, deal.II RK4 + DiscreteTime from oracle/cut1d.py (pinned by the
+    wave_0 golden)."""
+    import cut1d
+
+    m = O.Mesh(dim, p, n, -1.21, 1.21)
+    X = m.vertex_coords()
+    u0 = np.ones(m.n_dofs)
+    for d in range(dim):
+        u0 = u0 * np.cos(0.75 * np.pi * X[d] / 1.21 + 0.2 * d)
+    N = m.n_dofs
+
+    def f(t, y):
+        return np.concatenate([y[N:], m.kron_mass_inverse(m.wave_rhs(y[:N], impl=True, nitsche=nitsche))])
+
+    y = np.concatenate([u0, np.zeros(N)])
+    dt = cfl * (2.42 / n)
+    time = cut1d.DiscreteTime(0.0, 1e9, dt)
+    for _ in range(steps):
+        y = cut1d.rk4_step(f, time.t, time.next_step_size(), y)
+        time.advance()
+    return y
+
+
+def test_wave_driver_is_built():
+    assert os.access(WAVE_APP, os.X_OK), "build() must compile the wave driver"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,p,n,steps,nitsche", [(1, 3, 40, 5, 0.0), (2, 5, 16, 3, 0.0), (3, 7, 8, 2, 0.0),
+                                                   (2, 3, 12, 3, 15.0)])
+def test_wave_driver_rk4_matches_oracle(tmp_path, dim, p, n, steps, nitsche):
+    out = tmp_path / "uv.bin"
+    r = subprocess.run([WAVE_APP, str(dim), str(p), str(n), str(steps), "0.05", str(out), str(nitsche)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    uv = np.fromfile(out, dtype=np.float64)
+    ref = wave_oracle(dim, p, n, steps, 0.05, nitsche)
+    assert uv.shape == ref.shape
+    N = len(ref) // 2
+    for a, b in ((uv[:N], ref[:N]), (uv[N:], ref[N:])):
+        assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-10

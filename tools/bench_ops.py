@@ -9,7 +9,10 @@
 Algorithmic bytes: 16 B per DoF and application (read once, write once).
 One JSON line per (config, operator) on stdout.
 
-    python tools/bench_ops.py [--configs C3,C4,C2] [--iters 10]
+    python tools/bench_ops.py [--configs C3,C4,C2] [--iters 10] [--ops apply,mass_solve,rk_step]
+
+rk_step: one device-resident RK4 step (gdm_amd.problem: 4 x (compute_rhs +
+mass solve) + fused stage updates); C4 = the wave-rk stage of BASELINE C4.
 """
 import argparse
 import json
@@ -55,6 +58,31 @@ def main():
             print(json.dumps({"config": name, "op": opname, "kind": c["kind"], "dim": c["dim"], "p": c["p"],
                               "n_dofs": n, "ms": ms, "dof_per_s": n / (ms * 1e-3), "alg_GBps": gbs,
                               "frac_8TBps": gbs / 8000.0}), flush=True)
+        if "rk_step" in args.ops.split(","):
+            # one full RK4 step (4 x (compute_rhs + mass solve) + the fused stage updates), device-resident
+            from gdm_amd import AdvectionProblem, WaveProblem
+
+            if c["kind"] == "wave":
+                prob = WaveProblem(op)
+                prob.u.copy_(src[:n])
+            else:
+                prob = AdvectionProblem(op, op.FN_SINE_PRODUCT, [1.0, 0.15, -0.05, 1.0, 1.0, 1.0, 0.3, 0.0, 0.7])
+                prob.u.copy_(src[:n])
+            dt = 1e-4
+            for _ in range(2):
+                prob.step(0.0, dt)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for i in range(args.iters):
+                prob.step(i * dt, dt)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.iters
+            print(json.dumps({"config": name, "op": "rk_step", "kind": c["kind"], "dim": c["dim"], "p": c["p"],
+                              "n_dofs": n, "ms": ms, "stage_ms": ms / 4, "dof_updates_per_s": 4 * n / (ms * 1e-3)}),
+                  flush=True)
+            del prob
         del op, src, dst, bc
         torch.cuda.empty_cache()
 
