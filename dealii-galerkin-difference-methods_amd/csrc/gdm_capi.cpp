@@ -117,6 +117,10 @@ struct gdm_op {
   std::vector<double> cst3_host[3];
   double *bc_tab = nullptr;  // gdm_eval_boundary: per-face 1D factor tables
   int bc_tab_ld = 0;
+  // periodicity constraints (system.h:427-463): scratch copy of the input for
+  // distribute; CG work vectors and the Jacobi inverse diagonal
+  double *pscratch = nullptr;
+  double *cg_r = nullptr, *cg_p = nullptr, *cg_Ap = nullptr, *cg_z = nullptr, *cg_invdiag = nullptr;
   std::vector<Face> faces;
   double *face_tmp = nullptr;
   int64_t face_tmp_size = 0;
@@ -767,7 +771,16 @@ int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int
     if (!(mesh->hi[d] > mesh->lo[d])) return fail(GDM_ERR_ARG, "empty box");
   }
   if (mesh->n_ranks < 1 || mesh->rank < 0 || mesh->rank >= mesh->n_ranks) return fail(GDM_ERR_ARG, "bad rank");
-  if (mesh->periodic != 0) return fail(GDM_ERR_UNSUPPORTED, "periodic constraints are not supported by the device path yet");
+  if (mesh->periodic & ~((1 << dim) - 1)) return fail(GDM_ERR_ARG, "periodic bit beyond dim");
+  if (mesh->periodic) {
+    if (mesh->n_ranks != 1) return fail(GDM_ERR_UNSUPPORTED, "periodic constraints: single rank only");
+    if (kind == GDM_OP_ADVECTION)
+      return fail(GDM_ERR_UNSUPPORTED,
+                  "periodic constraints with the advection face terms (use the convective form of "
+                  "prototypes/advection_01_gdm.cc)");
+    if (kind == GDM_OP_WAVE && n_params > 0 && params && params[0] > 0.0)
+      return fail(GDM_ERR_UNSUPPORTED, "periodic constraints with box Nitsche terms");
+  }
   if ((kind == GDM_OP_ADVECTION || kind == GDM_OP_CONVECTIVE) && (n_params < dim || !params))
     return fail(GDM_ERR_ARG, "advection needs the constant field a (dim values)");
   gdm_op *op = new (std::nothrow) gdm_op();
@@ -845,12 +858,38 @@ int gdm_op_use_own_stream(gdm_op *op) {
   return GDM_OK;
 }
 
+namespace {
+
+// constraints.distribute(src) into a scratch copy, the operator, then the
+// condensation of distribute_local_to_global (system.h:427-463 constraints:
+// x_{last} = x_{first} per periodic direction; rows of constrained DoFs zero)
+void periodic_stencil(gdm_op *op, bool mass, const double *src, double *dst) {
+  const int64_t n = op->layout.n_local;
+  if (!op->pscratch) op->pscratch = keep(op, dev_upload(std::vector<double>((size_t)std::max<int64_t>(n, 1), 0.0)));
+  hip_check(hipMemcpyAsync(op->pscratch, src, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+  const int64_t N[3] = {op->N[0], op->N[1], op->N[2]};
+  for (int d = 0; d < op->dim; ++d)
+    if (op->mesh.periodic & (1 << d)) hip_check(gdmk_launch_periodic(op->pscratch, N, d, 0, op->stream), "distribute");
+  hip_check(launch_stencil(op, mass, op->pscratch, dst), "stencil launch");
+  for (int d = op->dim - 1; d >= 0; --d)
+    if (op->mesh.periodic & (1 << d)) hip_check(gdmk_launch_periodic(dst, N, d, 1, op->stream), "condense");
+}
+
+void any_stencil(gdm_op *op, bool mass, const double *src, double *dst) {
+  if (op->mesh.periodic)
+    periodic_stencil(op, mass, src, dst);
+  else
+    hip_check(launch_stencil(op, mass, src, dst), "stencil launch");
+}
+
+}  // namespace
+
 int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const double *bc_values) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
-  hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned), "stencil launch");
+  any_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned);
   if (bc_values) launch_boundary_data(op, bc_values, dst_owned);
   return GDM_OK;
   GDM_GUARD_END
@@ -861,6 +900,7 @@ int gdm_apply_planes(gdm_op *op, const double *src_local, double *dst_owned, int
   if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
   if (op->part_axis != 2 && (plane_begin > op->layout.owned_plane_begin || plane_end < op->layout.owned_plane_end))
     return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_planes: plane sub-ranges need a 3D mesh");
+  if (op->mesh.periodic) return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_planes: periodic constraints");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, plane_begin, plane_end),
@@ -884,7 +924,7 @@ int gdm_mass_apply(gdm_op *op, const double *src_local, double *dst_owned) {
   if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
-  hip_check(launch_stencil(op, true, src_local, dst_owned), "stencil launch");
+  any_stencil(op, true, src_local, dst_owned);
   return GDM_OK;
   GDM_GUARD_END
 }
@@ -893,6 +933,8 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   if (op->mesh.n_ranks != 1)
     return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve: the exact Kronecker inverse is single-rank in this version");
+  if (op->mesh.periodic)
+    return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve: periodic constraints couple the line ends; use gdm_mass_solve_cg");
   if (!rhs_owned || !x_owned) return fail(GDM_ERR_ARG, "NULL vector");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
@@ -937,6 +979,112 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
   if (X > 1) pass(0, 0, X, 1, Y * Z, 1, 0, "mass x");           // x lines: contiguous rows of length X
   if (in != x_owned)
     hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_mass_solve_cg(gdm_op *op, const double *rhs_owned, double *x_owned, double rel_tol, double abs_tol,
+                      int max_it, int precond, int *its_host, double *res_host) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->mesh.n_ranks != 1) return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_cg: single rank in this version");
+  if (!rhs_owned || !x_owned || rhs_owned == x_owned) return fail(GDM_ERR_ARG, "rhs and x: distinct device vectors");
+  if (precond != 0 && precond != 1) return fail(GDM_ERR_ARG, "precond: 0 identity, 1 Jacobi");
+  if (max_it < 0) return fail(GDM_ERR_ARG, "max_it < 0");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  const int64_t n = op->layout.n_owned;
+  auto vec = [&](double *&v) {
+    if (!v) v = keep(op, dev_upload(std::vector<double>((size_t)std::max<int64_t>(n, 1), 0.0)));
+  };
+  vec(op->cg_r);
+  vec(op->cg_p);
+  vec(op->cg_Ap);
+  vec(op->cg_z);
+  if (precond == 1 && !op->cg_invdiag) {
+    // diag of the condensed mass P^T M P = kron_d diag(P_d^T M_d P_d); constrained rows 1
+    std::vector<double> dg[3];
+    for (int d = 0; d < 3; ++d) {
+      if (d >= op->dim) {
+        dg[d].assign(1, 1.0);
+        continue;
+      }
+      const unsigned nc = (unsigned)op->mesh.n_subdivisions[d];
+      const double h = (op->mesh.hi[d] - op->mesh.lo[d]) / nc;
+      const gdm::Band M = gdm::assemble_1d(op->p, nc, h).M;
+      dg[d].resize(M.n);
+      for (int i = 0; i < M.n; ++i) dg[d][i] = M(i, i);
+      if (op->mesh.periodic & (1 << d)) {
+        dg[d][0] += M(M.n - 1, M.n - 1) + M(0, M.n - 1) + M(M.n - 1, 0);
+        dg[d][M.n - 1] = 1.0;
+      }
+    }
+    std::vector<double> inv((size_t)n);
+    const int64_t N0 = op->N[0], N1 = op->N[1];
+    for (int64_t g = 0; g < n; ++g) {
+      const int64_t i0 = g % N0, i1 = (g / N0) % N1, i2 = g / (N0 * N1);
+      bool constrained = false;
+      const int64_t id[3] = {i0, i1, i2};
+      for (int d = 0; d < op->dim; ++d)
+        if ((op->mesh.periodic & (1 << d)) && id[d] == op->N[d] - 1) constrained = true;
+      inv[g] = constrained ? 1.0 : 1.0 / (dg[0][i0] * dg[1][op->dim > 1 ? i1 : 0] * dg[2][op->dim > 2 ? i2 : 0]);
+    }
+    op->cg_invdiag = keep(op, dev_upload(inv));
+  }
+  auto dot = [&](const double *a, const double *b) {
+    double r = 0.0;
+    if (gdm_vec_dot(op, n, a, b, &r) != GDM_OK) throw std::runtime_error("dot");
+    return r;
+  };
+  auto precondition = [&](const double *r, double *z) {
+    if (precond == 1)
+      hip_check(gdmk_launch_vmul(n, op->cg_invdiag, r, z, op->stream), "jacobi");
+    else
+      hip_check(hipMemcpyAsync(z, r, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+  };
+  // SolverCG with ReductionControl(max_it, abs_tol, rel_tol): r = b - A x
+  any_stencil(op, true, x_owned, op->cg_r);
+  hip_check(gdmk_launch_axpby(n, 1.0, rhs_owned, -1.0, op->cg_r, op->stream), "axpby");
+  double res = std::sqrt(dot(op->cg_r, op->cg_r));
+  const double tol = std::max(abs_tol, rel_tol * res);
+  int it = 0;
+  if (res > tol) {
+    precondition(op->cg_r, op->cg_z);
+    hip_check(hipMemcpyAsync(op->cg_p, op->cg_z, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+    double rz = dot(op->cg_r, op->cg_z);
+    while (true) {
+      if (it >= max_it) {
+        if (its_host) *its_host = it;
+        if (res_host) *res_host = res;
+        return fail(GDM_ERR_STATE, "gdm_mass_solve_cg: max_it reached (SolverControl::NoConvergence)");
+      }
+      ++it;
+      any_stencil(op, true, op->cg_p, op->cg_Ap);
+      const double alpha = rz / dot(op->cg_p, op->cg_Ap);
+      hip_check(gdmk_launch_axpby(n, alpha, op->cg_p, 1.0, x_owned, op->stream), "axpby");
+      hip_check(gdmk_launch_axpby(n, -alpha, op->cg_Ap, 1.0, op->cg_r, op->stream), "axpby");
+      res = std::sqrt(dot(op->cg_r, op->cg_r));
+      if (res <= tol) break;
+      precondition(op->cg_r, op->cg_z);
+      const double rz_new = dot(op->cg_r, op->cg_z);
+      hip_check(gdmk_launch_axpby(n, 1.0, op->cg_z, rz_new / rz, op->cg_p, op->stream), "axpby");
+      rz = rz_new;
+    }
+  }
+  if (its_host) *its_host = it;
+  if (res_host) *res_host = res;
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_constraints_distribute(gdm_op *op, double *v_owned) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (!op->mesh.periodic) return GDM_OK;
+  if (!v_owned) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  const int64_t N[3] = {op->N[0], op->N[1], op->N[2]};
+  for (int d = 0; d < op->dim; ++d)
+    if (op->mesh.periodic & (1 << d)) hip_check(gdmk_launch_periodic(v_owned, N, d, 0, op->stream), "distribute");
   return GDM_OK;
   GDM_GUARD_END
 }

@@ -1,5 +1,6 @@
 // gdm_rk.h -- device-side argument blocks and launchers of gdm_rk.hip
-// (device-resident RK stage updates and boundary-function evaluation).
+// (device-resident RK stage updates, boundary-function evaluation,
+// periodicity constraints and the vector kernels of the matrix-free CG).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,6 +36,11 @@ extern "C" {
 // gdm_rk.hip: acc_out = acc_in + beta k; Y = y + alpha k (Y may be NULL)
 hipError_t gdmk_launch_rk_update(int64_t n, double beta, const double *k, const double *acc_in, double *acc_out,
                                  double alpha, const double *y, double *Y, hipStream_t st);
+// periodicity constraints along direction d (global layout): mode 0
+// distribute v[last] = v[first], mode 1 condense v[first] += v[last], v[last] = 0
+hipError_t gdmk_launch_periodic(double *v, const int64_t N[3], int d, int mode, hipStream_t st);
+// y = w .* x
+hipError_t gdmk_launch_vmul(int64_t n, const double *w, const double *x, double *y, hipStream_t st);
 // tab: scratch of n_faces * 3 * ld * 2 doubles, ld >= max(Q0, Q1)
 hipError_t gdmk_launch_bc_eval(const gdmk::BcGeom &g, const gdmk::BcFn &f, double t, int derivative, double *out,
                                double *tab, int ld, hipStream_t st);

@@ -123,6 +123,37 @@ __global__ void __launch_bounds__(256) bc_face_kernel(BcGeom g, BcFace F, BcFn f
   *o = r;
 }
 
+// Periodicity constraints of System::make_periodicity_constraints
+// (include/gdm/system.h:427-463): vertex N_d - 1 of direction d is
+// constrained to vertex 0.  mode 0 = distribute (v[i1] = v[i0]), mode 1 =
+// condense a residual (v[i0] += v[i1], v[i1] = 0).  One thread per vertex of
+// the face x_d = 0; global lexicographic layout (x fastest).
+__global__ void __launch_bounds__(256) periodic_kernel(double *v, int64_t N0, int64_t N1, int64_t N2, int d,
+                                                       int mode) {
+  const int64_t N[3] = {N0, N1, N2};
+  const int64_t stride[3] = {1, N0, N0 * N1};
+  const int a = d == 0 ? 1 : 0, b = d == 2 ? 1 : 2;  // the two other directions
+  const int64_t nf = N[a] * N[b];
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < nf; f += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ia = f % N[a], ib = f / N[a];
+    const int64_t i0 = ia * stride[a] + ib * stride[b];
+    const int64_t i1 = i0 + (N[d] - 1) * stride[d];
+    if (mode == 0) {
+      v[i1] = v[i0];
+    } else {
+      v[i0] += v[i1];
+      v[i1] = 0.0;
+    }
+  }
+}
+
+// x *= w elementwise (Jacobi preconditioner application, w = 1 / diag)
+__global__ void __launch_bounds__(256) vmul_kernel(int64_t n, const double *__restrict__ w,
+                                                   const double *__restrict__ x, double *__restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = w[i] * x[i];
+}
+
 }  // namespace gdmk
 
 extern "C" hipError_t gdmk_launch_rk_update(int64_t n, double beta, const double *k, const double *acc_in,
@@ -147,5 +178,21 @@ extern "C" hipError_t gdmk_launch_bc_eval(const gdmk::BcGeom &g, const gdmk::BcF
     hipLaunchKernelGGL(gdmk::bc_face_kernel, dim3((unsigned)((F.Q[0] + 255) / 256), (unsigned)F.Q[1]), dim3(256), 0,
                        st, g, F, f, t, derivative, tab + (size_t)fi * 3 * ld * 2, ld, out);
   }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gdmk_launch_periodic(double *v, const int64_t N[3], int d, int mode, hipStream_t st) {
+  const int a = d == 0 ? 1 : 0, b = d == 2 ? 1 : 2;
+  const int64_t nf = N[a] * N[b];
+  const int64_t blocks = std::min<int64_t>((nf + 255) / 256, 4096);
+  hipLaunchKernelGGL(gdmk::periodic_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, st, v, N[0],
+                     N[1], N[2], d, mode);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gdmk_launch_vmul(int64_t n, const double *w, const double *x, double *y, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(gdmk::vmul_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n, w, x, y);
   return hipGetLastError();
 }

@@ -146,6 +146,21 @@ class GdmOperator:
         check(self.lib.gdm_mass_solve(self.h, _ptr(rhs_owned), _ptr(x_owned)), "gdm_mass_solve")
         return x_owned
 
+    def mass_solve_cg(self, rhs_owned, x_owned, rel_tol=1e-8, abs_tol=1e-10, max_it=100, precond=1):
+        """SolverCG on the matrix-free (condensed) mass: returns (iterations, residual)"""
+        self._check_sizes(None, rhs_owned)
+        self._check_sizes(None, x_owned)
+        its, res = ctypes.c_int(0), ctypes.c_double(0.0)
+        check(self.lib.gdm_mass_solve_cg(self.h, _ptr(rhs_owned), _ptr(x_owned), float(rel_tol), float(abs_tol),
+                                         int(max_it), int(precond), ctypes.byref(its), ctypes.byref(res)),
+              "gdm_mass_solve_cg")
+        return its.value, res.value
+
+    def distribute(self, v_owned):
+        """constraints.distribute (periodicity constraints; no-op otherwise)"""
+        check(self.lib.gdm_constraints_distribute(self.h, _ptr(v_owned)), "gdm_constraints_distribute")
+        return v_owned
+
     def mass_solve_lines(self, axis, v, n_lines, stride, A, B, C):
         """In-place 1D mass solves along `axis` (gdm_mass_solve_lines)."""
         check(self.lib.gdm_mass_solve_lines(self.h, int(axis), _ptr(v), int(n_lines), int(stride), int(A), int(B),

@@ -155,3 +155,56 @@ class AdvectionProblem:
             n += 1
             time.advance()
         return n
+
+
+class Advection01:
+    """prototypes/advection_01_gdm.cc:62-282 (use_mass_lumping = false) on the
+    device: periodicity constraints in every direction (:107-110), the
+    convective form cell_i -= (a . grad u_q) phi_i JxW (:164-206) on the
+    distributed stage vector, SolverCG + PreconditionJacobi with
+    ReductionControl(100, 1e-10, 1e-8) from a zero initial guess (:208-217),
+    RK_CLASSIC_FOURTH_ORDER + DiscreteTime, constraints.distribute after
+    every step (:268).  `op` is a "convective" operator with periodic = all
+    directions."""
+
+    def __init__(self, op):
+        if op.mesh.n_ranks != 1:
+            raise GdmError("Advection01: single rank")
+        self.op = op
+        self.u = op.new_vector(False)
+        self._acc, self._Y, self._k = (op.new_vector(False) for _ in range(3))
+        self.cg_iterations = []
+
+    def rhs(self, U, out):
+        op = self.op
+        op.apply(U, self._r_tmp())  # distributes a copy of U, condenses the result
+        out.zero_()
+        its, _ = op.mass_solve_cg(self._r, out, rel_tol=1e-8, abs_tol=1e-10, max_it=100, precond=1)
+        self.cg_iterations.append(its)
+        return out
+
+    def _r_tmp(self):
+        if not hasattr(self, "_r"):
+            self._r = self.op.new_vector(False)
+        return self._r
+
+    def step(self, t, h):
+        op, y = self.op, self.u
+        acc, Y, k = self._acc, self._Y, self._k
+        stage = y
+        for s in range(4):
+            self.rhs(stage, k)
+            last = s == 3
+            op.rk_update(h * RK4_B[s], k, y if s == 0 else acc, y if last else acc,
+                         0.0 if last else h * RK4_A[s], None if last else y, None if last else Y)
+            stage = Y
+        op.distribute(y)
+
+    def run(self, start_t, end_t, dt, max_steps=None):
+        time = DiscreteTime(start_t, end_t, dt)
+        n = 0
+        while not time.is_at_end() and (max_steps is None or n < max_steps):
+            self.step(time.t, time.next_step_size())
+            n += 1
+            time.advance()
+        return n

@@ -84,7 +84,12 @@ typedef struct {
   int32_t n_subdivisions[3]; /* cells per direction                          */
   double lo[3], hi[3];       /* box (subdivided_hyper_cube/_rectangle)       */
   int32_t n_ranks, rank;     /* slab partition along the last coordinate     */
-  int32_t periodic;          /* bit d: periodic constraints in direction d   */
+  int32_t periodic;          /* bit d: periodic constraints in direction d
+                                (System::make_periodicity_constraints, system.h:427-463:
+                                vertex N_d - 1 := vertex 0; gdm_apply / gdm_mass_apply
+                                distribute the input and condense the result, the
+                                constrained rows are zero; single rank; not with the
+                                advection face terms or box Nitsche) */
 } gdm_mesh_desc;
 
 /* Local vector layout of one rank.  Device vectors are stored
@@ -148,8 +153,25 @@ int gdm_apply_planes(gdm_op *op, const double *src_local, double *dst_owned, int
 int gdm_add_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned);
 /* dst_owned = M src_local */
 int gdm_mass_apply(gdm_op *op, const double *src_local, double *dst_owned);
-/* x_owned = M^-1 rhs_owned (exact Kronecker inverse; single rank) */
+/* x_owned = M^-1 rhs_owned (exact Kronecker inverse; single rank; not with
+ * periodic constraints: gdm_mass_solve_cg) */
 int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned);
+
+/* x_owned = M^-1 rhs_owned by SolverCG on the matrix-free mass operator with
+ * ReductionControl(max_it, abs_tol, rel_tol) semantics, the solve of
+ * prototypes/advection_01_gdm.cc:208-217 (PreconditionJacobi, rel 1e-8) and of
+ * *Problem::solve (advection/problem.h:251-261); precond 0 = identity,
+ * 1 = Jacobi (diagonal of the condensed mass).  x_owned is the initial guess
+ * (the reference starts from zero); *its_host = SolverControl::last_step();
+ * GDM_ERR_STATE when max_it is reached.  Works with periodic constraints (the
+ * condensed operator: constrained rows zero).  Single rank. */
+int gdm_mass_solve_cg(gdm_op *op, const double *rhs_owned, double *x_owned, double rel_tol, double abs_tol,
+                      int max_it, int precond, int *its_host, double *res_host);
+
+/* AffineConstraints::distribute of the periodicity constraints
+ * (advection_01_gdm.cc:158, 268): v[last vertex of d] = v[first] for every
+ * periodic direction d; no-op without periodic constraints. */
+int gdm_constraints_distribute(gdm_op *op, double *v_owned);
 
 /* In-place banded-Cholesky solve with the 1D mass matrix of reference
  * direction `axis` (0 = x, 1 = y, 2 = z) along n_lines lines of full length
