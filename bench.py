@@ -8,9 +8,16 @@ GPU, plus achieved HBM GB/s of the dominant kernel against the 8 TB/s roofline.
 
 One step = ghost-plane exchange (N > 1) + fused Kronecker stencil kernel
 (volume term + outflow traces) + inflow boundary-data kernels, on inputs that
-are resident in HBM.  Weak scaling: each rank owns one 512-plane z-slab of a
-512 x 512 x 512N vertex grid partitioned with the reference's slab formula
-(system.h:720-757); --strong keeps the global grid at 512^3 instead.
+are resident in HBM.  N = 1: 512^3 DoFs (BASELINE C3).  N > 1: strong scaling
+on the same 512^3 global grid (C3 "512^3 DoFs, 8 x MI355X"), z-slabs of the
+reference's formula (system.h:720-757); --weak gives every rank a 512-plane
+slab of a 512 x 512 x 512N grid instead.
+
+At N = 1 the line also carries the other two per-stage operations of the RK
+loop, timed the same way (HIP events on the operator's stream): the exact
+mass inverse (roofline.mass_solve) and one device-resident RK4 stage
+(compute_rhs + mass solve + fused stage updates + device boundary data,
+rk4_stage_ms).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -37,7 +44,9 @@ def parse():
     ap.add_argument("--n", type=int, default=511, help="cells per direction per GPU slab (vertices = n + 1)")
     ap.add_argument("--p", type=int, default=5)
     ap.add_argument("--kind", default="advection", choices=["advection", "wave", "mass"])
-    ap.add_argument("--strong", action="store_true", help="fixed global grid instead of one slab per GPU")
+    ap.add_argument("--strong", action="store_true", help="(default for N > 1) fixed 512^3 global grid")
+    ap.add_argument("--weak", action="store_true", help="one 512-plane slab per GPU instead of a fixed global grid")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0: min(16, cpu_count))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cells", type=int, default=24, help="cells per direction of the CPU-baseline sample")
     ap.add_argument("--pmc", default=os.environ.get("GDM_BENCH_PMC", "1"), help="collect HBM PMC traffic (1/0)")
@@ -45,34 +54,97 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(p, n_cells):
+def cpu_baseline(p, n_cells, threads):
     """Reference algorithm (per-cell FEValues loop of stiffness.h:345-532) from
-    the CPU restatement in oracle/, single thread, on a bounded sample."""
+    the CPU restatement in oracle/, on a bounded sample: `threads` host
+    threads, each running the cell loop over its own z-slab of cells into a
+    private vector (ctypes releases the GIL; the reference's MPI ranks do the
+    same with one slab each), summed; plus the 1-thread rate and the mass
+    solve the reference runs per stage (CSR mass + SolverCG with
+    PreconditionJacobi to rel 1e-14, advection/problem.h:236-267) at 24^3
+    cells."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from concurrent.futures import ThreadPoolExecutor
+
     import numpy as np
     import oracle as O
 
-    m = O.Mesh(3, p, n_cells, 0.0, 1.0)
-    u = np.random.default_rng(20251010).uniform(-1, 1, m.n_dofs)
-    bc = np.random.default_rng(1).uniform(-1, 1, m.n_boundary_points())
     a = (1.0, 0.15, -0.05)
     O.Mesh(3, p, p + 1).advection_rhs(a, np.zeros((p + 2) ** 3), None)  # load the library
+    m = O.Mesh(3, p, n_cells, 0.0, 1.0)
+    u = np.random.default_rng(20251010).uniform(-1, 1, m.n_dofs)
+    bounds = [(n_cells * t // threads, n_cells * (t + 1) // threads) for t in range(threads)]
+    bcs = [np.random.default_rng(1 + t).uniform(-1, 1, max(m.n_boundary_points(cb, ce), 1)) for t, (cb, ce) in
+           enumerate(bounds)]
+    outs = [np.zeros(m.n_dofs) for _ in range(threads)]
+
+    def part(t):
+        cb, ce = bounds[t]
+        outs[t][:] = 0.0
+        m.advection_rhs(a, u, bcs[t], cb=cb, ce=ce, rhs=outs[t])
+
+    def timed(fn, budget):
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            fn()
+            reps += 1
+            if time.perf_counter() - t0 > budget:
+                break
+        return (time.perf_counter() - t0) / reps, reps
+
+    with ThreadPoolExecutor(threads) as ex:
+        def all_parts():
+            list(ex.map(part, range(threads)))
+            np.sum(outs, axis=0)
+
+        dt_n, reps_n = timed(all_parts, 10.0)
+    bc1 = np.random.default_rng(3).uniform(-1, 1, m.n_boundary_points())
+    dt_1, reps_1 = timed(lambda: m.advection_rhs(a, u, bc1), 5.0)
+    # mass solve: CSR + CG(Jacobi) to rel 1e-14 (the reference's per-stage solve).  The CSR matrix is
+    # the Kronecker product of the oracle's 1D mass matrices (equal to the cell-assembled matrix up to
+    # round-off; the oracle's cell assembly itself takes minutes at this size)
+    import scipy.sparse as sps
+
+    mm = O.Mesh(3, p, 24, 0.0, 1.0)
+    M1 = []
+    for d in range(3):
+        band = mm.matrices_1d(d)[0]
+        N = band.shape[0]
+        M1.append(sps.diags([band[max(0, -k + p):N - max(0, k - p) + max(0, -k + p), k][: N - abs(k - p)]
+                             for k in range(2 * p + 1)], [k - p for k in range(2 * p + 1)], shape=(N, N)))
+    A = sps.kron(M1[2], sps.kron(M1[1], M1[0])).tocsr()
+    A.sort_indices()
+    rp, cols, vals = A.indptr.astype(np.int64), A.indices.astype(np.int64), A.data
+    r = np.random.default_rng(4).uniform(-1, 1, mm.n_dofs)
     t0 = time.perf_counter()
-    reps = 0
-    while True:
-        m.advection_rhs(a, u, bc)
-        reps += 1
-        if time.perf_counter() - t0 > 10.0:
-            break
-    dt = (time.perf_counter() - t0) / reps
+    _, its = O.cg(rp, cols, vals, r, precond=1, max_it=1000, abs_tol=1e-20, rel_tol=1e-14)
+    dt_m = time.perf_counter() - t0
     return {
-        "value": m.n_dofs / dt,
+        "value": m.n_dofs / dt_n,
         "unit": "DoF-updates/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": "3D p=%d advection compute_rhs, reference per-cell algorithm (oracle/gdm_oracle.c), "
-                  "%d^3 cells = %d DoFs, %d application(s) in %.1f s, 1 thread" % (p, n_cells, m.n_dofs, reps, dt * reps),
+        "cpu": _cpu_model(),
+        "sample": "3D p=%d advection compute_rhs, reference per-cell algorithm (oracle/gdm_oracle.c), %d^3 cells = "
+                  "%d DoFs, %d z-slabs on %d threads, %d application(s) in %.1f s"
+                  % (p, n_cells, m.n_dofs, threads, threads, reps_n, dt_n * reps_n),
+        "value_1_thread": m.n_dofs / dt_1,
+        "sample_1_thread": "same mesh, %d application(s), 1 thread" % reps_1,
+        "mass_solve": {"value": mm.n_dofs / dt_m, "unit": "DoF/s (one M^-1 r)", "cores": 1, "cg_iterations": int(its),
+                       "sample": "24^3 cells p=%d: CSR mass (%d nnz) + SolverCG/Jacobi rel 1e-14, 1 thread"
+                                 % (p, len(vals))},
     }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def pmc_traffic(args):
@@ -129,7 +201,8 @@ def main():
     from gdm_amd.distributed import HaloExchange, apply_overlapped
 
     p, n = args.p, args.n
-    nz_cells = n if (args.strong or world == 1) else (n + 1) * world - 1
+    weak = args.weak and not args.strong
+    nz_cells = (n + 1) * world - 1 if (weak and world > 1) else n
     n_sub = (n, n, nz_cells)
     hi = (1.0, 1.0, nz_cells / n)  # uniform h = 1/n
     a = (1.0, 0.15, -0.05)        # advection_01_gdm.cc:37-41
@@ -199,13 +272,37 @@ def main():
         return
 
     achieved = BYTES_PER_DOF * lay["n_owned"] / (kern_ms * 1e-3) / 1e9
+    mass = stage_ms = None
+    if world == 1:
+        # the exact mass inverse (gdm_mass_solve; HIP events on the op stream) and one device-resident RK4
+        # stage of the advection problem (AdvectionProblem.step / 4)
+        ms = op.time_op(2, dst, src[:lay["n_owned"]], None, 10)
+        mass = {"bound": "hbm", "kernel": "mass3_strided_kernel (z, y) + mass3_rows_kernel (x)",
+                "achieved": BYTES_PER_DOF * lay["n_owned"] / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": BYTES_PER_DOF * lay["n_owned"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel_ms": ms,
+                "algorithmic_bytes_per_launch": BYTES_PER_DOF * lay["n_owned"]}
+        if args.kind == "advection":
+            from gdm_amd import AdvectionProblem
+
+            prob = AdvectionProblem(op, op.FN_SINE_PRODUCT, [1.0, 0.15, -0.05, 1.0, 1.0, 1.0, 0.3, 0.0, 0.7])
+            prob.u.copy_(src[:lay["n_owned"]])
+            prob.step(0.0, 1e-4)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for i in range(3):
+                prob.step(i * 1e-4, 1e-4)
+            e1.record()
+            torch.cuda.synchronize()
+            stage_ms = e0.elapsed_time(e1) / 12.0
+            del prob
     traffic = None
     if world == 1 and str(args.pmc) == "1":
         traffic = pmc_traffic(args)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(p, args.cpu_cells)
+            cpu = cpu_baseline(p, args.cpu_cells, args.cpu_threads or min(16, os.cpu_count() or 1))
         except Exception as e:  # the baseline never blocks the GPU line
             cpu = {"value": None, "error": str(e)}
     out = {
@@ -217,7 +314,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong" if args.strong else "weak",
+        "scaling": "weak" if (weak and world > 1) else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: u ~ U[-1,1) seeded, stage boundary values ~ U[-1,1); inputs resident in HBM",
@@ -241,7 +338,9 @@ def main():
             "traffic": traffic,
             "kernel_ms": kern_ms,
             "algorithmic_bytes_per_launch": BYTES_PER_DOF * lay["n_owned"],
+            "mass_solve": mass,
         },
+        "rk4_stage_ms": stage_ms,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
