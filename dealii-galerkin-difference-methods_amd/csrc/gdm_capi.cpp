@@ -72,6 +72,7 @@ struct Face {
   int64_t n_points = 0;
   FaceDir t0, t1;
   int64_t base = 0;       // owned index of node (i0 = 0, i1 = t1.node_begin)
+  double *T = nullptr;    // step-1 scratch of this face (faces run concurrently)
 };
 
 }  // namespace
@@ -82,6 +83,11 @@ int gdm_internal_set_error(int code, const char *msg) { return fail(code, msg); 
 struct gdm_op {
   int device = 0;
   hipStream_t own_stream = nullptr, stream = nullptr;
+  // fork / join of gdm_apply: the z-wall stencil launch and the inflow face
+  // step 1 run on side_stream, filling the tail of the interior launch
+  hipStream_t side_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool concurrent = true;  // GDM_SERIAL=1: everything on one stream
   gdm_mesh_desc mesh{};
   int kind = 0, p = 1, dim = 1;
   int N[3] = {1, 1, 1};        // vertices per reference direction
@@ -139,6 +145,9 @@ void free_op(gdm_op *op) {
   if (!op) return;
   for (void *ptr : op->allocations) (void)hipFree(ptr);
   if (op->own_stream) (void)hipStreamDestroy(op->own_stream);
+  if (op->side_stream) (void)hipStreamDestroy(op->side_stream);
+  if (op->ev_fork) (void)hipEventDestroy(op->ev_fork);
+  if (op->ev_join) (void)hipEventDestroy(op->ev_join);
   delete op;
 }
 
@@ -545,6 +554,11 @@ void build_faces(gdm_op *op) {
     F.base = node_d * stride[d] + (int64_t)F.t0.node_begin * F.t0.stride + (int64_t)F.t1.node_begin * F.t1.stride -
              own_off;
     max_tmp = std::max<int64_t>(max_tmp, (int64_t)F.t1.Q * (F.t0.node_end - F.t0.node_begin));
+    if (F.scale != 0.0) {
+      const int64_t tsz = std::max<int64_t>(1, (int64_t)F.t1.Q * (F.t0.node_end - F.t0.node_begin));
+      hip_check(hipMalloc(&F.T, sizeof(double) * tsz), "hipMalloc");
+      keep(op, F.T);
+    }
     op->faces.push_back(F);
   }
   op->layout.n_bc_points = offset;
@@ -573,7 +587,8 @@ void build_faces(gdm_op *op) {
 
 // Output planes [zb, ze) of the owned range (3D: z planes; the full owned
 // range otherwise).  dst is the owned vector; only those planes are written.
-hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst, int zb = -1, int ze = -1) {
+hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst, int zb = -1, int ze = -1,
+                          hipStream_t wall_stream = nullptr) {
   const gdm_layout &L = op->layout;
   gdmk::StencilArgs a{};
   a.src = src;
@@ -674,10 +689,13 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
   a.zchunk = std::max(1, std::max(i0 - zb, ze - i1));
   a.nchunk0 = i0 > zb ? 1 : 0;
   if (i0 <= zb && i1 >= ze) return hipSuccess;
-  return gdmk_launch_stencil8(p, bk, false, a, op->stream);
+  return gdmk_launch_stencil8(p, bk, false, a, wall_stream ? wall_stream : op->stream);
 }
 
-void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned) {
+// phase 0: both steps on op->stream; 1: step 1 (bc values -> per-face T) on
+// stream `st`; 2: step 2 (T -> dst) on op->stream
+void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
+                          hipStream_t st = nullptr) {
   if (op->kind != GDM_OP_ADVECTION) return;
   {
     for (const Face &F : op->faces) {
@@ -704,13 +722,14 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
       fa.p = op->p;
       fa.ncell0_total = F.t0.ncell_total;
       fa.cell0_begin = F.t0.cell_begin;
-      fa.T = op->face_tmp;
+      fa.T = F.T ? F.T : op->face_tmp;
       fa.dst = dst_owned;
       fa.base = F.base;
       fa.stride0 = F.t0.stride;
       fa.stride1 = F.t1.stride;
       fa.scale = F.scale;
-      hip_check(gdmk_launch_face(fa, op->stream), "face launch");
+      fa.phase = phase;
+      hip_check(gdmk_launch_face(fa, phase == 1 && st ? st : op->stream), "face launch");
     }
   }
 }
@@ -807,6 +826,10 @@ int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int
   hip_check(hipSetDevice(device), "hipSetDevice");
   hip_check(hipStreamCreateWithFlags(&op->own_stream, hipStreamNonBlocking), "hipStreamCreate");
   op->stream = op->own_stream;
+  hip_check(hipStreamCreateWithFlags(&op->side_stream, hipStreamNonBlocking), "hipStreamCreate");
+  hip_check(hipEventCreateWithFlags(&op->ev_fork, hipEventDisableTiming), "hipEventCreate");
+  hip_check(hipEventCreateWithFlags(&op->ev_join, hipEventDisableTiming), "hipEventCreate");
+  if (const char *env = std::getenv("GDM_SERIAL")) op->concurrent = std::atoi(env) == 0;
   build_layout(op);
   build_tables(op);
   build_faces(op);
@@ -836,6 +859,7 @@ int gdm_op_destroy(gdm_op *op) {
   if (!op) return GDM_OK;
   (void)hipSetDevice(op->device);
   if (op->own_stream) (void)hipStreamSynchronize(op->own_stream);
+  if (op->side_stream) (void)hipStreamSynchronize(op->side_stream);
   free_op(op);
   return GDM_OK;
 }
@@ -889,8 +913,21 @@ int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const doub
   if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
-  any_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned);
-  if (bc_values) launch_boundary_data(op, bc_values, dst_owned);
+  if (op->concurrent && !op->mesh.periodic) {
+    // fork: z-wall launch + face step 1 on the side stream fill the tail of the
+    // interior launch; join before face step 2 adds into dst
+    hip_check(hipEventRecord(op->ev_fork, op->stream), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(op->side_stream, op->ev_fork, 0), "hipStreamWaitEvent");
+    hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, -1, -1, op->side_stream),
+              "stencil launch");
+    if (bc_values) launch_boundary_data(op, bc_values, dst_owned, 1, op->side_stream);
+    hip_check(hipEventRecord(op->ev_join, op->side_stream), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(op->stream, op->ev_join, 0), "hipStreamWaitEvent");
+    if (bc_values) launch_boundary_data(op, bc_values, dst_owned, 2);
+  } else {
+    any_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned);
+    if (bc_values) launch_boundary_data(op, bc_values, dst_owned);
+  }
   return GDM_OK;
   GDM_GUARD_END
 }

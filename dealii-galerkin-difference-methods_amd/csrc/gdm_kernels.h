@@ -72,6 +72,7 @@ struct FaceArgs {
   double *dst;
   int64_t base, stride0, stride1;  // dst offset of node (i0_begin, i1_begin)
   double scale;
+  int phase;  // 0: both steps, 1: step 1 only (writes T), 2: step 2 only (T -> dst)
 };
 
 constexpr int FACE_CHUNK = 256;  // t0 nodes per workgroup of the face row kernel

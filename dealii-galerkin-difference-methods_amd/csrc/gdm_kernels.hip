@@ -1479,7 +1479,7 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
     // cell form of step 1, then the usual step 2
     const int rpb = 4;
     dim3 g1c((f.Q1 + rpb - 1) / rpb);
-    switch (f.p) {
+    if (f.phase != 2) switch (f.p) {
 #define GDM_FACE_CELL(PP)                                                                                            \
   case PP:                                                                                                         \
     hipLaunchKernelGGL(face_cell_step1_kernel<PP>, g1c, dim3(512), cell_lds, st, f.U, f.Q0, f.Q1, rpb, f.i0_begin, \
@@ -1490,8 +1490,9 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
       default: return hipErrorInvalidValue;
     }
     dim3 g2((n0 + 255) / 256, f.i1_end - f.i1_begin);
-    hipLaunchKernelGGL(face_step2_kernel, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1,
-                       f.wmax1, f.dst, f.base, f.stride0, f.stride1, f.scale);
+    if (f.phase != 1)
+      hipLaunchKernelGGL(face_step2_kernel, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1,
+                         f.wmax1, f.dst, f.base, f.stride0, f.stride1, f.scale);
     return hipGetLastError();
   }
   dim3 b(256);
@@ -1501,7 +1502,9 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
   if (row_bytes > 48 * 1024) return hipErrorInvalidValue;  // <= (FACE_CHUNK + 2p) (p + 1) doubles in practice
   dim3 g1((n0 + FACE_CHUNK - 1) / FACE_CHUNK, (f.Q1 + rows - 1) / rows);
   const size_t lds = row_bytes * rows;
-  if (rows == 4)
+  if (f.phase == 2)
+    ;
+  else if (rows == 4)
     hipLaunchKernelGGL(face_step1_kernel<4>, g1, dim3(FACE_CHUNK), lds, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
                        f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
   else if (rows == 2)
@@ -1511,8 +1514,9 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
     hipLaunchKernelGGL(face_step1_kernel<1>, g1, dim3(FACE_CHUNK), lds, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
                        f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
   dim3 g2((n0 + 255) / 256, f.i1_end - f.i1_begin);
-  hipLaunchKernelGGL(face_step2_kernel, g2, b, 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1,
-                     f.dst, f.base, f.stride0, f.stride1, f.scale);
+  if (f.phase != 1)
+    hipLaunchKernelGGL(face_step2_kernel, g2, b, 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1,
+                       f.dst, f.base, f.stride0, f.stride1, f.scale);
   return hipGetLastError();
 }
 
