@@ -151,6 +151,42 @@ void free_op(gdm_op *op) {
   delete op;
 }
 
+// diag of the condensed mass P^T M P = kron_d diag(P_d^T M_d P_d) on the owned
+// DoFs (global lexicographic order from the owned plane range); constrained
+// rows of periodic directions 1
+std::vector<double> mass_diagonal_owned(const gdm_op *op) {
+  std::vector<double> dg[3];
+  for (int d = 0; d < 3; ++d) {
+    if (d >= op->dim) {
+      dg[d].assign(1, 1.0);
+      continue;
+    }
+    const unsigned nc = (unsigned)op->mesh.n_subdivisions[d];
+    const double h = (op->mesh.hi[d] - op->mesh.lo[d]) / nc;
+    const gdm::Band M = gdm::assemble_1d(op->p, nc, h).M;
+    dg[d].resize(M.n);
+    for (int i = 0; i < M.n; ++i) dg[d][i] = M(i, i);
+    if (op->mesh.periodic & (1 << d)) {
+      dg[d][0] += M(M.n - 1, M.n - 1) + M(0, M.n - 1) + M(M.n - 1, 0);
+      dg[d][M.n - 1] = 1.0;
+    }
+  }
+  const int64_t n = op->layout.n_owned;
+  const int64_t g0 = (int64_t)op->layout.owned_plane_begin * op->layout.plane_size;
+  std::vector<double> out((size_t)n);
+  const int64_t N0 = op->N[0], N1 = op->N[1];
+  for (int64_t l = 0; l < n; ++l) {
+    const int64_t g = g0 + l;
+    const int64_t i0 = g % N0, i1 = (g / N0) % N1, i2 = g / (N0 * N1);
+    bool constrained = false;
+    const int64_t id[3] = {i0, i1, i2};
+    for (int d = 0; d < op->dim; ++d)
+      if ((op->mesh.periodic & (1 << d)) && id[d] == op->N[d] - 1) constrained = true;
+    out[l] = constrained ? 1.0 : dg[0][i0] * dg[1][op->dim > 1 ? i1 : 0] * dg[2][op->dim > 2 ? i2 : 0];
+  }
+  return out;
+}
+
 template <typename T>
 T *keep(gdm_op *op, T *ptr) {
   op->allocations.push_back((void *)ptr);
@@ -864,6 +900,101 @@ int gdm_op_destroy(gdm_op *op) {
   return GDM_OK;
 }
 
+int gdm_halo_plan(const gdm_mesh_desc *mesh, gdm_halo *out) {
+  if (!mesh || !out) return fail(GDM_ERR_ARG, "NULL argument");
+  const int dim = mesh->dim, p = mesh->fe_degree;
+  if (dim < 1 || dim > 3 || p < 1) return fail(GDM_ERR_ARG, "bad mesh");
+  if (mesh->n_ranks < 1 || mesh->rank < 0 || mesh->rank >= mesh->n_ranks) return fail(GDM_ERR_ARG, "bad rank");
+  const int q = dim - 1;
+  const unsigned ncq = (unsigned)mesh->n_subdivisions[q];
+  const int nq = (int)ncq + 1;
+  int64_t plane = 1;
+  for (int d = 0; d < q; ++d) plane *= mesh->n_subdivisions[d] + 1;
+  auto lay = [&](int r, int &pb, int &pe, int &gb, int &ga) {
+    const gdm::Slab s = gdm::slab_partition(ncq, (unsigned)mesh->n_ranks, (unsigned)r);
+    pb = (int)s.plane_begin;
+    pe = std::max(pb, (int)s.plane_end);
+    gb = pe > pb ? std::min(p, pb) : 0;
+    ga = pe > pb ? std::min(p, nq - pe) : 0;
+  };
+  const int r = mesh->rank;
+  int pb, pe, gb, ga;
+  lay(r, pb, pe, gb, ga);
+  gdm_halo h{};
+  h.rank_below = (r > 0 && pe > pb) ? r - 1 : -1;
+  h.rank_above = (r + 1 < mesh->n_ranks && pe > pb) ? r + 1 : -1;
+  h.owned_offset = (int64_t)gb * plane;
+  if (h.rank_below >= 0) {
+    int nb, ne, ngb, nga;
+    lay(r - 1, nb, ne, ngb, nga);
+    if (nga > pe - pb) return fail(GDM_ERR_UNSUPPORTED, "slab thinner than the halo");
+    h.send_below_offset = (int64_t)gb * plane;
+    h.send_below_count = (int64_t)nga * plane;
+    h.recv_below_offset = 0;
+    h.recv_below_count = (int64_t)gb * plane;
+  }
+  if (h.rank_above >= 0) {
+    int nb, ne, ngb, nga;
+    lay(r + 1, nb, ne, ngb, nga);
+    if (ngb > pe - pb) return fail(GDM_ERR_UNSUPPORTED, "slab thinner than the halo");
+    h.send_above_offset = (int64_t)(gb + (pe - pb) - ngb) * plane;
+    h.send_above_count = (int64_t)ngb * plane;
+    h.recv_above_offset = (int64_t)(gb + (pe - pb)) * plane;
+    h.recv_above_count = (int64_t)ga * plane;
+  }
+  // the reference's ghost layer: DoF boxes of the cells next to the owned
+  // cell slab (one ghost cell layer, system.h:767-771) minus the owned planes
+  {
+    const gdm::Slab s = gdm::slab_partition(ncq, (unsigned)mesh->n_ranks, (unsigned)r);
+    int lo = pb, hi = pe;
+    if (s.cell_end > s.cell_begin) {
+      const unsigned c0 = s.cell_begin > 0 ? s.cell_begin - 1 : 0;
+      const unsigned c1 = std::min(ncq, s.cell_end + 1);
+      for (unsigned c = c0; c < c1; ++c) {
+        const int off = (int)gdm::box_offset(c, (unsigned)p, ncq);
+        lo = std::min(lo, off);
+        hi = std::max(hi, off + p + 1);
+      }
+    }
+    h.dealii_ghost_planes_below = pb - lo;
+    h.dealii_ghost_planes_above = hi - pe;
+  }
+  *out = h;
+  return GDM_OK;
+}
+
+int gdm_mass_diagonal(gdm_op *op, double *diag_owned) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_owned > 0 && !diag_owned) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  const std::vector<double> d = mass_diagonal_owned(op);
+  if (!d.empty())
+    hip_check(hipMemcpyAsync(diag_owned, d.data(), sizeof(double) * d.size(), hipMemcpyHostToDevice, op->stream),
+              "copy");
+  hip_check(hipStreamSynchronize(op->stream), "sync");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_vec_pointwise_mult(gdm_op *op, int64_t n, const double *w, const double *x, double *y) {
+  if (!op || (n > 0 && (!w || !x || !y))) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  hip_check(gdmk_launch_vmul(n, w, x, y, op->stream), "vmul");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_memcpy_d2d(gdm_op *op, void *dst, const void *src, size_t bytes) {
+  if (!op || (bytes && (!dst || !src))) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  if (bytes) hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, op->stream), "copy");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
 int gdm_op_layout(const gdm_op *op, gdm_layout *out) {
   if (!op || !out) return fail(GDM_ERR_ARG, "op/out is NULL");
   *out = op->layout;
@@ -1038,33 +1169,8 @@ int gdm_mass_solve_cg(gdm_op *op, const double *rhs_owned, double *x_owned, doub
   vec(op->cg_Ap);
   vec(op->cg_z);
   if (precond == 1 && !op->cg_invdiag) {
-    // diag of the condensed mass P^T M P = kron_d diag(P_d^T M_d P_d); constrained rows 1
-    std::vector<double> dg[3];
-    for (int d = 0; d < 3; ++d) {
-      if (d >= op->dim) {
-        dg[d].assign(1, 1.0);
-        continue;
-      }
-      const unsigned nc = (unsigned)op->mesh.n_subdivisions[d];
-      const double h = (op->mesh.hi[d] - op->mesh.lo[d]) / nc;
-      const gdm::Band M = gdm::assemble_1d(op->p, nc, h).M;
-      dg[d].resize(M.n);
-      for (int i = 0; i < M.n; ++i) dg[d][i] = M(i, i);
-      if (op->mesh.periodic & (1 << d)) {
-        dg[d][0] += M(M.n - 1, M.n - 1) + M(0, M.n - 1) + M(M.n - 1, 0);
-        dg[d][M.n - 1] = 1.0;
-      }
-    }
-    std::vector<double> inv((size_t)n);
-    const int64_t N0 = op->N[0], N1 = op->N[1];
-    for (int64_t g = 0; g < n; ++g) {
-      const int64_t i0 = g % N0, i1 = (g / N0) % N1, i2 = g / (N0 * N1);
-      bool constrained = false;
-      const int64_t id[3] = {i0, i1, i2};
-      for (int d = 0; d < op->dim; ++d)
-        if ((op->mesh.periodic & (1 << d)) && id[d] == op->N[d] - 1) constrained = true;
-      inv[g] = constrained ? 1.0 : 1.0 / (dg[0][i0] * dg[1][op->dim > 1 ? i1 : 0] * dg[2][op->dim > 2 ? i2 : 0]);
-    }
+    std::vector<double> inv = mass_diagonal_owned(op);
+    for (double &v : inv) v = 1.0 / v;
     op->cg_invdiag = keep(op, dev_upload(inv));
   }
   auto dot = [&](const double *a, const double *b) {

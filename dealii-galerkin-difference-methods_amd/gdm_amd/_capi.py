@@ -34,6 +34,27 @@ class MeshDesc(ctypes.Structure):
     ]
 
 
+class Halo(ctypes.Structure):
+    _fields_ = [
+        ("rank_below", ctypes.c_int32),
+        ("rank_above", ctypes.c_int32),
+        ("owned_offset", ctypes.c_int64),
+        ("send_below_offset", ctypes.c_int64),
+        ("send_below_count", ctypes.c_int64),
+        ("recv_below_offset", ctypes.c_int64),
+        ("recv_below_count", ctypes.c_int64),
+        ("send_above_offset", ctypes.c_int64),
+        ("send_above_count", ctypes.c_int64),
+        ("recv_above_offset", ctypes.c_int64),
+        ("recv_above_count", ctypes.c_int64),
+        ("dealii_ghost_planes_below", ctypes.c_int32),
+        ("dealii_ghost_planes_above", ctypes.c_int32),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Layout(ctypes.Structure):
     _fields_ = [
         ("n_dofs_global", ctypes.c_int64),
@@ -75,6 +96,10 @@ def load():
         "gdm_op_create": [ctypes.POINTER(MeshDesc), i32, P, i32, i32, ctypes.POINTER(P)],
         "gdm_op_destroy": [P],
         "gdm_op_layout": [P, ctypes.POINTER(Layout)],
+        "gdm_halo_plan": [ctypes.POINTER(MeshDesc), ctypes.POINTER(Halo)],
+        "gdm_mass_diagonal": [P, P],
+        "gdm_memcpy_d2d": [P, P, P, ctypes.c_size_t],
+        "gdm_vec_pointwise_mult": [P, i64, P, P, P],
         "gdm_op_set_stream": [P, P],
         "gdm_op_use_own_stream": [P],
         "gdm_apply": [P, P, P, P],

@@ -3,7 +3,7 @@
 // (gdm/hip/operators.h), in the shape of
 // applications/advection/advection-app.cc:86-154 + problem.h:31-102.
 //
-//   advection_app DIM P N STEPS CFL OUT [DEVICE] [DEVBC]
+//   advection_app DIM P N STEPS CFL OUT [DEVICE] [DEVBC] [NRANKS]
 //
 // Manufactured solution u(x, t) = prod_d sin(2 pi (x_d - a_d t) + 0.3 d) on
 // [0, 1]^dim with a = (1, 0.15, -0.05) (prototypes/advection_01_gdm.cc:37-41);
@@ -11,12 +11,17 @@
 // values after STEPS RK4 steps to OUT (raw little-endian doubles, reference
 // global order) and prints one line per step with |u|_2.  DEVBC = 1 evaluates
 // g and dg/dt on the device (GDM_FN_SINE_PRODUCT with the same parameters)
-// instead of the host callbacks.
+// instead of the host callbacks.  NRANKS > 1 runs the multi-rank path: one
+// thread per rank (z-slabs of system.h:720-757, all on DEVICE), ghost planes
+// and dots through GDM::HIP::ThreadGroup (an MPI communicator's role), the
+// distributed CG mass solve; OUT holds the ranks' owned values in rank order.
 #include <gdm/hip/operators.h>
+#include <gdm/hip/thread_communicator.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <thread>
 
 namespace {
 
@@ -43,7 +48,7 @@ double dg_dt(const GDM::HIP::Point &x, double t) {
 }
 
 template <int dim>
-int run(int p, int n, int steps, double cfl, const char *out, int device, int devbc) {
+GDM::HIP::Parameters<dim> make_params(int p, int n, double cfl, int device, int devbc) {
   GDM::HIP::Parameters<dim> params;
   params.fe_degree = p;
   params.n_subdivisions_1D = n;
@@ -61,9 +66,58 @@ int run(int p, int n, int steps, double cfl, const char *out, int device, int de
     params.boundary_function = GDM_FN_SINE_PRODUCT;
     params.boundary_function_params = {kA[0], kA[1], kA[2], 1.0, 1.0, 1.0, 0.0, 0.3, 0.6};
   }
-  GDM::HIP::AdvectionProblem<dim> problem(params);
-  const unsigned int done = problem.run(steps);
-  const std::vector<double> u = problem.get_solution();
+  return params;
+}
+
+template <int dim>
+int run(int p, int n, int steps, double cfl, const char *out, int device, int devbc, int n_ranks) {
+  std::vector<double> u;
+  unsigned int done = 0;
+  if (n_ranks <= 1) {
+    GDM::HIP::AdvectionProblem<dim> problem(make_params<dim>(p, n, cfl, device, devbc));
+    done = problem.run(steps);
+    u = problem.get_solution();
+  } else {
+    gdm_mesh_desc mesh{};
+    mesh.dim = dim;
+    mesh.fe_degree = p;
+    for (int d = 0; d < 3; ++d) {
+      mesh.n_subdivisions[d] = d < dim ? n : 1;
+      mesh.lo[d] = 0.0;
+      mesh.hi[d] = 1.0;
+    }
+    mesh.n_ranks = n_ranks;
+    GDM::HIP::ThreadGroup group(n_ranks);
+    std::vector<gdm_halo> plans(n_ranks);
+    for (int r = 0; r < n_ranks; ++r) {
+      mesh.rank = r;
+      GDM::HIP::check(gdm_halo_plan(&mesh, &plans[r]), "gdm_halo_plan");
+    }
+    group.set_plans(plans);
+    std::vector<std::vector<double>> parts(n_ranks);
+    std::vector<std::string> errors(n_ranks);
+    std::vector<unsigned int> steps_done(n_ranks, 0);
+    std::vector<std::thread> threads;
+    for (int r = 0; r < n_ranks; ++r)
+      threads.emplace_back([&, r] {
+        try {
+          GDM::HIP::Parameters<dim> params = make_params<dim>(p, n, cfl, device, devbc);
+          params.n_ranks = n_ranks;
+          params.rank = r;
+          GDM::HIP::ThreadGroup::Rank comm(group, r, mesh);
+          GDM::HIP::AdvectionProblem<dim> problem(params, &comm);
+          steps_done[r] = problem.run(steps);
+          parts[r] = problem.get_solution();
+        } catch (const std::exception &e) {
+          errors[r] = e.what();
+          std::fprintf(stderr, "rank %d: %s\n", r, e.what());
+          std::_Exit(1);  // a failed rank would leave the others blocked in a barrier
+        }
+      });
+    for (auto &t : threads) t.join();
+    for (int r = 0; r < n_ranks; ++r) u.insert(u.end(), parts[r].begin(), parts[r].end());
+    done = steps_done[0];
+  }
   double s = 0.0;
   for (double v : u) s += v * v;
   std::printf("steps %u  |u|_2 %.15e\n", done, std::sqrt(s));
@@ -83,11 +137,12 @@ int main(int argc, char **argv) {
   const double cfl = std::atof(argv[5]);
   const int device = argc > 7 ? std::atoi(argv[7]) : 0;
   const int devbc = argc > 8 ? std::atoi(argv[8]) : 0;
+  const int n_ranks = argc > 9 ? std::atoi(argv[9]) : 1;
   try {
     switch (dim) {
-      case 1: return run<1>(p, n, steps, cfl, argv[6], device, devbc);
-      case 2: return run<2>(p, n, steps, cfl, argv[6], device, devbc);
-      case 3: return run<3>(p, n, steps, cfl, argv[6], device, devbc);
+      case 1: return run<1>(p, n, steps, cfl, argv[6], device, devbc, n_ranks);
+      case 2: return run<2>(p, n, steps, cfl, argv[6], device, devbc, n_ranks);
+      case 3: return run<3>(p, n, steps, cfl, argv[6], device, devbc, n_ranks);
       default: std::fprintf(stderr, "dim must be 1, 2 or 3\n"); return 2;
     }
   } catch (const GDM::HIP::Error &e) {

@@ -157,6 +157,21 @@ struct BlockVector {
   }
 };
 
+// What a multi-rank problem needs from its communicator (MPI_COMM_WORLD in
+// the reference): the ghost-plane exchange of update_ghost_values
+// (advection/stiffness.h:343) over the ranges of gdm_halo_plan, and
+// Utilities::MPI::sum for the dots of the distributed CG.  An MPI rank
+// implements it with MPI_Isend / MPI_Irecv (GPU-aware) or ncclSend / ncclRecv
+// on those ranges; gdm/hip/thread_communicator.h runs ranks
+// as threads of one process for the tests.
+class Communicator {
+ public:
+  virtual ~Communicator() = default;
+  // fill the ghost planes of `local` (engine-local layout of `op`) from the slab neighbours
+  virtual void update_ghost_values(gdm_op *op, DeviceVector &local) = 0;
+  virtual double sum(double local_value) = 0;
+};
+
 // RK_CLASSIC_FOURTH_ORDER (deal.II TimeStepping): c_i, a_{i,i-1}, b_i
 struct ClassicRK4 {
   static constexpr double c[4] = {0.0, 0.5, 0.5, 1.0};
@@ -323,12 +338,63 @@ class MassMatrixOperator {
     const MassMatrixOperator &M;
   };
   SparseMatrix get_sparse_matrix() const { return SparseMatrix(*this); }
+
+  // Multi-rank solve(M, x, b) (problem.h:251-261): SolverCG with
+  // ReductionControl(max_it, abs_tol, rel_tol) and the Jacobi preconditioner
+  // on the matrix-free mass, ghost planes and dots through `comm`; x (owned)
+  // starts from zero like the reference's fresh result vector.  Returns the
+  // number of iterations (SolverControl::last_step).
+  unsigned int solve_distributed(double *x_owned, const double *b_owned, Communicator &comm, double rel_tol = 1e-14,
+                                 double abs_tol = 1e-20, unsigned int max_it = 1000) const {
+    const int64_t n = layout.n_owned;
+    if (cg_p.size() != (std::size_t)layout.n_local) {
+      cg_p.reinit(op, layout.n_local);
+      for (auto *v : {&cg_r, &cg_z, &cg_Ap, &cg_invdiag}) v->reinit(op, n);
+      check(gdm_mass_diagonal(op, cg_invdiag.get_values()), "gdm_mass_diagonal");
+      std::vector<double> d = cg_invdiag.download();
+      for (double &v : d) v = 1.0 / v;
+      cg_invdiag.upload(d);
+    }
+    const int64_t o = layout.ghost_planes_below * layout.plane_size;
+    double *p_owned = cg_p.get_values() + o;
+    auto dot = [&](const double *a, const double *b) {
+      double r = 0.0;
+      check(gdm_vec_dot(op, n, a, b, &r), "gdm_vec_dot");
+      return comm.sum(r);
+    };
+    check(gdm_vec_axpby(op, n, 0.0, b_owned, 0.0, x_owned), "gdm_vec_axpby");            // x = 0
+    check(gdm_vec_axpby(op, n, 1.0, b_owned, 0.0, cg_r.get_values()), "gdm_vec_axpby");  // r = b
+    double res = std::sqrt(dot(cg_r.get_values(), cg_r.get_values()));
+    const double tol = std::max(abs_tol, rel_tol * res);
+    unsigned int it = 0;
+    if (res <= tol) return 0;
+    check(gdm_vec_pointwise_mult(op, n, cg_invdiag.get_values(), cg_r.get_values(), cg_z.get_values()), "jacobi");
+    check(gdm_vec_axpby(op, n, 1.0, cg_z.get_values(), 0.0, p_owned), "gdm_vec_axpby");
+    double rz = dot(cg_r.get_values(), cg_z.get_values());
+    while (true) {
+      if (it >= max_it) throw Error("MassMatrixOperator::solve_distributed: SolverControl::NoConvergence");
+      ++it;
+      comm.update_ghost_values(op, cg_p);
+      check(gdm_mass_apply(op, cg_p.get_values(), cg_Ap.get_values()), "gdm_mass_apply");
+      const double alpha = rz / dot(p_owned, cg_Ap.get_values());
+      check(gdm_vec_axpby(op, n, alpha, p_owned, 1.0, x_owned), "gdm_vec_axpby");
+      check(gdm_vec_axpby(op, n, -alpha, cg_Ap.get_values(), 1.0, cg_r.get_values()), "gdm_vec_axpby");
+      res = std::sqrt(dot(cg_r.get_values(), cg_r.get_values()));
+      if (res <= tol) break;
+      check(gdm_vec_pointwise_mult(op, n, cg_invdiag.get_values(), cg_r.get_values(), cg_z.get_values()), "jacobi");
+      const double rz_new = dot(cg_r.get_values(), cg_z.get_values());
+      check(gdm_vec_axpby(op, n, 1.0, cg_z.get_values(), rz_new / rz, p_owned), "gdm_vec_axpby");
+      rz = rz_new;
+    }
+    return it;
+  }
   gdm_op *handle() const { return op; }
 
  private:
   const Discretization<dim> &discretization;
   gdm_op *op = nullptr;
   gdm_layout layout{};
+  mutable DeviceVector cg_p, cg_r, cg_z, cg_Ap, cg_invdiag;  // solve_distributed work vectors
 };
 
 // deal.II DiscreteTime: fixed steps, the last one shrunk to hit end_t or, when
@@ -360,13 +426,14 @@ class DiscreteTime {
 template <int dim>
 class AdvectionProblem {
  public:
-  explicit AdvectionProblem(const Parameters<dim> &params)
-      : params(params), mass_matrix_operator(discretization), stiffness_matrix_operator(discretization) {}
+  // comm: required for n_ranks > 1 (MPI_COMM_WORLD of the reference)
+  explicit AdvectionProblem(const Parameters<dim> &params, Communicator *comm = nullptr)
+      : params(params), comm(comm), mass_matrix_operator(discretization), stiffness_matrix_operator(discretization) {}
 
   // Runs to end_t (or max_steps); returns the number of steps.  The solution
   // is available through get_solution() (owned DoFs, reference global order).
   unsigned int run(unsigned int max_steps = ~0u) {
-    if (params.n_ranks != 1) throw Error("AdvectionProblem: the host RK driver is single-rank");
+    if (params.n_ranks != 1 && !comm) throw Error("AdvectionProblem: n_ranks > 1 needs a Communicator");
     discretization.reinit(params);
     mass_matrix_operator.reinit(params);
     stiffness_matrix_operator.reinit(params);
@@ -380,10 +447,19 @@ class AdvectionProblem {
     stiffness_matrix_operator.initialize_dof_vector(k);
     stiffness_matrix_operator.initialize_dof_vector(acc);
     stiffness_matrix_operator.initialize_dof_vector(stage);
-    const auto fu_rhs = [&](double time, const BlockVector &y, BlockVector &result) {
+    if (params.n_ranks != 1) rhs_tmp.reinit(stiffness_matrix_operator.handle(), stiffness_matrix_operator.get_layout().n_owned);
+    const auto fu_rhs = [&](double time, BlockVector &y, BlockVector &result) {
+      if (params.n_ranks != 1) comm->update_ghost_values(stiffness_matrix_operator.handle(), y.block(1));
       stiffness_matrix_operator.compute_rhs(result, y, time);
       double *r = stiffness_matrix_operator.owned(result.block(1));
-      mass_matrix_operator.solve(r, r);
+      if (params.n_ranks == 1) {
+        mass_matrix_operator.solve(r, r);
+      } else {
+        check(gdm_memcpy_d2d(stiffness_matrix_operator.handle(), rhs_tmp.get_values(), r,
+                             sizeof(double) * rhs_tmp.size()),
+              "gdm_memcpy_d2d");
+        mass_matrix_operator.solve_distributed(r, rhs_tmp.get_values(), *comm);
+      }
     };
     DiscreteTime time(params.start_t, params.end_t, delta_t);
     unsigned int n = 0;
@@ -391,7 +467,7 @@ class AdvectionProblem {
       stiffness_matrix_operator.initialize_time_step(solution, time.get_current_time());  // evaluate bc
       const double t0 = time.get_current_time(), h = time.get_next_step_size();
       for (int s = 0; s < 4; ++s) {
-        fu_rhs(t0 + ClassicRK4::c[s] * h, s == 0 ? solution : stage, k);
+        fu_rhs(t0 + ClassicRK4::c[s] * h, s == 0 ? solution : stage, k);  // ghosts of the stage exchanged
         for (unsigned int bl = 0; bl < 2; ++bl)
           rk4_stage_update(s, h, k.block(bl), solution.block(bl), acc.block(bl), stage.block(bl));
       }
@@ -401,7 +477,13 @@ class AdvectionProblem {
     return n;
   }
 
-  std::vector<double> get_solution() const { return solution.block(1).download(); }
+  // owned DoF values (reference global order of the owned planes)
+  std::vector<double> get_solution() const {
+    const gdm_layout &L = stiffness_matrix_operator.get_layout();
+    std::vector<double> v = solution.block(1).download();
+    const int64_t o = L.ghost_planes_below * L.plane_size;
+    return std::vector<double>(v.begin() + o, v.begin() + o + L.n_owned);
+  }
   const BlockVector &get_solution_vector() const { return solution; }
 
  private:
@@ -428,10 +510,12 @@ class AdvectionProblem {
   }
 
   Parameters<dim> params;
+  Communicator *comm = nullptr;
   Discretization<dim> discretization;
   MassMatrixOperator<dim> mass_matrix_operator;
   StiffnessMatrixOperator<dim> stiffness_matrix_operator;
   BlockVector solution;
+  DeviceVector rhs_tmp;
 };
 
 }  // namespace HIP

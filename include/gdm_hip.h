@@ -117,6 +117,32 @@ typedef struct {
                                      cells only (stiffness.h:40-160)                  */
 } gdm_layout;
 
+/* Ghost-plane exchange of one rank: owner-computes needs the
+ * p vertex planes next to the slab from each z-neighbour (the reference's
+ * update_ghost_values + compress(add), advection/stiffness.h:343, 605).  All
+ * ranges are in elements of the rank's engine-local vector (gdm_layout);
+ * every range is contiguous.  The caller moves them with its own
+ * communicator (MPI_Isend/Irecv on device pointers with a GPU-aware MPI,
+ * ncclSend/ncclRecv, or torch.distributed, gdm_amd/distributed.py):
+ *   send [send_below_offset, + send_below_count) to rank_below, which
+ *   receives it into its [recv_above_offset, + recv_above_count), and the
+ *   mirror image towards rank_above.
+ * deal.II's LinearAlgebra::distributed::Vector stores [owned | ghosts sorted]
+ * with the reference's ghost layer (one ghost cell layer: dealii_ghost_planes_
+ * below / _above planes, system.h:657-688, 767-771) -- fewer than the p planes
+ * owner-computes reads -- so the engine vector is a separate buffer: its owned
+ * block starts at owned_offset and equals deal.II's owned block element for
+ * element (the reference's global lexicographic order). */
+typedef struct {
+  int32_t rank_below, rank_above; /* -1: none */
+  int64_t owned_offset;           /* = ghost_planes_below * plane_size */
+  int64_t send_below_offset, send_below_count;
+  int64_t recv_below_offset, recv_below_count;
+  int64_t send_above_offset, send_above_count;
+  int64_t recv_above_offset, recv_above_count;
+  int32_t dealii_ghost_planes_below, dealii_ghost_planes_above;
+} gdm_halo;
+
 /* params (n_params):
  *   GDM_OP_MASS        : none
  *   GDM_OP_ADVECTION   : a_x, a_y, a_z               (constant field)
@@ -130,6 +156,8 @@ int gdm_get_device_count(int *n);
 int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int n_params, int device,
                   gdm_op **out);
 int gdm_op_destroy(gdm_op *op);
+/* the exchange plan of mesh->rank (pure host function: no device, no op) */
+int gdm_halo_plan(const gdm_mesh_desc *mesh, gdm_halo *out);
 int gdm_op_layout(const gdm_op *op, gdm_layout *out);
 /* launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream;
  * NULL is the HIP null stream); gdm_op_use_own_stream restores the operator's
@@ -167,6 +195,15 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned);
  * condensed operator: constrained rows zero).  Single rank. */
 int gdm_mass_solve_cg(gdm_op *op, const double *rhs_owned, double *x_owned, double rel_tol, double abs_tol,
                       int max_it, int precond, int *its_host, double *res_host);
+
+/* diag_owned (device) = the diagonal of the (condensed) mass matrix on the
+ * owned DoFs: the PreconditionJacobi of prototypes/advection_01_gdm.cc:211
+ * and the diagonal a distributed CG preconditions with (constrained rows 1). */
+int gdm_mass_diagonal(gdm_op *op, double *diag_owned);
+/* y = w .* x elementwise (a diagonal preconditioner application) */
+int gdm_vec_pointwise_mult(gdm_op *op, int64_t n, const double *w, const double *x, double *y);
+/* device-to-device copy on the operator's stream */
+int gdm_memcpy_d2d(gdm_op *op, void *dst, const void *src, size_t bytes);
 
 /* AffineConstraints::distribute of the periodicity constraints
  * (advection_01_gdm.cc:158, 268): v[last vertex of d] = v[first] for every

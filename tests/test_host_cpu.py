@@ -239,3 +239,56 @@ def test_distributed_mass_solve_gloo(world, dim, p, n):
     for _, off, v in res:
         x[off:off + len(v)] = v
     assert np.linalg.norm(x - ref) / np.linalg.norm(ref) < 1e-12
+
+
+def _plan(dim, p, n_sub, n_ranks, rank):
+    m = _capi.MeshDesc()
+    m.dim, m.fe_degree = dim, p
+    for d in range(3):
+        m.n_subdivisions[d] = n_sub[d] if d < dim else 1
+        m.lo[d], m.hi[d] = 0.0, 1.0
+    m.n_ranks, m.rank, m.periodic = n_ranks, rank, 0
+    h = _capi.Halo()
+    _capi.check(_capi.load().gdm_halo_plan(ctypes.byref(m), ctypes.byref(h)), "gdm_halo_plan")
+    return h.as_dict()
+
+
+@pytest.mark.parametrize("dim,p,n_sub", [(3, 5, (20, 9, 511)), (3, 7, (8, 8, 255)), (2, 5, (30, 100)),
+                                         (3, 3, (6, 6, 40))])
+@pytest.mark.parametrize("n_ranks", [2, 3, 4, 8])
+def test_halo_plan_matches_exchange(dim, p, n_sub, n_ranks):
+    """gdm_halo_plan (pure host ABI) describes exactly the ranges the
+    torch.distributed exchange moves (gdm_amd.distributed.HaloExchange), the
+    sends of one rank land in the receives of its neighbour, and the
+    reference's deal.II ghost layer (system.h:657-688, 767-771: the DoF boxes
+    of one ghost cell layer) is reported for the adapter."""
+    nl = n_sub[dim - 1]
+    plane = int(np.prod([n_sub[d] + 1 for d in range(dim - 1)]))
+    plans = [_plan(dim, p, n_sub, n_ranks, r) for r in range(n_ranks)]
+    m = O.Mesh(dim, p, list(n_sub))
+    for r, h in enumerate(plans):
+        me = layout(nl, n_ranks, r, plane, p)
+        assert h["owned_offset"] == me["ghost_planes_below"] * plane
+        if r > 0:
+            lo = plans[r - 1]
+            assert h["rank_below"] == r - 1 and lo["rank_above"] == r
+            assert h["send_below_count"] == lo["recv_above_count"]
+            assert h["recv_below_count"] == lo["send_above_count"]
+            assert h["recv_below_offset"] == 0
+            assert h["send_below_offset"] == h["owned_offset"]
+        else:
+            assert h["rank_below"] == -1
+        if r + 1 < n_ranks:
+            assert h["rank_above"] == r + 1
+            assert h["recv_above_offset"] == me["n_local"] - h["recv_above_count"]
+            assert h["send_above_offset"] + h["send_above_count"] == h["owned_offset"] + me["n_owned"]
+        # deal.II ghost planes = locally active planes (DoF boxes of owned + one ghost cell layer) - owned
+        pb, pe, cb, ce = slab(nl, n_ranks, r)
+        lo_c, hi_c = max(cb - 1, 0), min(ce + 1, nl)
+        planes = set()
+        for c in range(lo_c, hi_c):
+            cell = [0] * (dim - 1) + [c]
+            idx = sum(ci * int(np.prod([n_sub[e] for e in range(d)])) for d, ci in enumerate(cell))
+            planes |= {int(g) // plane for g in m.cell_dofs(idx)}
+        assert h["dealii_ghost_planes_below"] == len([q for q in planes if q < pb])
+        assert h["dealii_ghost_planes_above"] == len([q for q in planes if q >= pe])
