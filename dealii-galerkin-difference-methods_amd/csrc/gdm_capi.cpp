@@ -18,6 +18,7 @@
 #include "../../include/gdm_hip.h"
 #include "gdm_coeffs.h"
 #include "gdm_kernels.h"
+#include "gdm_post.h"
 #include "gdm_rk.h"
 #include "gdm_setup.h"
 
@@ -122,6 +123,9 @@ struct gdm_op {
   int row_lo3[3] = {0, 0, 0}, row_hi3[3] = {0, 0, 0};
   std::vector<double> cst3_host[3];
   double *bc_tab = nullptr;  // gdm_eval_boundary: per-face 1D factor tables
+  // gdm_error_norms: shape values per category, per-workgroup partials, result
+  double *err_S = nullptr, *err_partial = nullptr;
+  static constexpr int n_err_partial = 1024;
   int bc_tab_ld = 0;
   // periodicity constraints (system.h:427-463): scratch copy of the input for
   // distribute; CG work vectors and the Jacobi inverse diagonal
@@ -1317,6 +1321,72 @@ int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_param
   }
   hip_check(gdmk_launch_bc_eval(g, fn, t, derivative ? 1 : 0, bc_values, op->bc_tab, op->bc_tab_ld, op->stream),
             "bc_eval");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_error_norms(gdm_op *op, const double *u_local, int fn_kind, const double *params, int n_params, double t,
+                    double *cell_errors, double *norms_host) {
+  if (!op || !norms_host) return fail(GDM_ERR_ARG, "NULL argument");
+  if (op->layout.n_local > 0 && !u_local) return fail(GDM_ERR_ARG, "NULL u_local");
+  const int need[3] = {1, 1 + op->dim, 9};
+  if (fn_kind < 0 || fn_kind > 2) return fail(GDM_ERR_ARG, "unknown gdm_fn_kind");
+  if (n_params < need[fn_kind] || (n_params > 0 && !params)) return fail(GDM_ERR_ARG, "too few function parameters");
+  if (op->p + 1 > 10) return fail(GDM_ERR_UNSUPPORTED, "fe_degree > 9");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  const int p = op->p, n1 = p + 1, q = op->dim - 1;
+  const gdm_layout &L = op->layout;
+  gdmk::ErrGeom g{};
+  g.dim = op->dim;
+  g.p = p;
+  std::vector<double> xq, wq;
+  gdm::gauss_unit(n1, xq, wq);
+  g.jxw = 1.0;
+  for (int d = 0; d < 3; ++d) {
+    const bool on = d < op->dim;
+    g.ncell[d] = on ? op->mesh.n_subdivisions[d] : 1;
+    g.cb[d] = 0;
+    g.ce[d] = g.ncell[d];
+    g.nb[d] = g.nq[d] = on ? n1 : 1;
+    g.lo[d] = on ? op->mesh.lo[d] : 0.0;
+    g.h[d] = on ? (op->mesh.hi[d] - op->mesh.lo[d]) / op->mesh.n_subdivisions[d] : 1.0;
+    if (on) g.jxw *= g.h[d];
+  }
+  g.cb[q] = L.cell_plane_begin;
+  g.ce[q] = L.cell_plane_end;
+  for (int k = 0; k < n1; ++k) {
+    g.xq[k] = xq[k];
+    g.wq[k] = wq[k];
+  }
+  g.N0 = op->N[0];
+  g.N1 = op->dim > 1 ? op->N[1] : 1;
+  g.base = (int64_t)(L.owned_plane_begin - L.ghost_planes_below) * L.plane_size;
+  gdmk::BcFn fn{};
+  fn.kind = fn_kind;
+  fn.dim = op->dim;
+  for (int i = 0; i < n_params && i < 12; ++i) fn.prm[i] = params[i];
+  if (!op->err_S) {
+    const int ncat = std::max(1, p);
+    std::vector<double> S((size_t)ncat * n1 * n1);
+    for (int c = 0; c < ncat; ++c)
+      for (int i = 0; i < n1; ++i)
+        for (int k = 0; k < n1; ++k) S[((size_t)c * n1 + i) * n1 + k] = gdm::shape_1d(p, c, i, xq[k], 0);
+    op->err_S = keep(op, dev_upload(S));
+    op->err_partial = keep(op, dev_upload(std::vector<double>((size_t)3 * op->n_err_partial + 3, 0.0)));
+  }
+  double out[3] = {0.0, 0.0, 0.0};
+  if (g.ce[q] > g.cb[q]) {
+    double *res = op->err_partial + 3 * op->n_err_partial;
+    hip_check(gdmk_launch_error_norms(g, fn, t, op->err_S, u_local, cell_errors, op->err_partial, op->n_err_partial,
+                                      res, op->stream),
+              "error_norms");
+    hip_check(hipMemcpyAsync(out, res, sizeof(out), hipMemcpyDeviceToHost, op->stream), "d2h");
+    hip_check(hipStreamSynchronize(op->stream), "sync");
+  }
+  norms_host[0] = out[0];
+  norms_host[1] = out[1];
+  norms_host[2] = std::sqrt(out[2]);
   return GDM_OK;
   GDM_GUARD_END
 }

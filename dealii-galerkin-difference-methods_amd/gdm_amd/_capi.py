@@ -114,6 +114,7 @@ def load():
         "gdm_vec_dot": [P, i64, P, P, ctypes.POINTER(d)],
         "gdm_vec_rk_update": [P, i64, d, P, P, P, d, P, P],
         "gdm_eval_boundary": [P, i32, P, i32, d, i32, P],
+        "gdm_error_norms": [P, P, i32, P, i32, d, P, P],
         "gdm_synchronize": [P],
         "gdm_malloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
         "gdm_free": [P, P],

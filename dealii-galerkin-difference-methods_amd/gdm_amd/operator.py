@@ -192,6 +192,30 @@ class GdmOperator:
                                          _ptr(out)), "gdm_eval_boundary")
         return out
 
+    def error_norms(self, u_local, fn_kind, params, t, cell_errors=None):
+        """(Linf, L1, L2) of u - f(t) over QGauss(p+1) on the owned cells
+        (advection/problem.h:269-425 postprocess, volume part); cell_errors
+        (device, n_owned_cells) receives integrate_difference's per-cell L2
+        errors (vector_tools.h:25-86).  Multi-rank callers reduce: max, sum,
+        sqrt(sum of squares)."""
+        if u_local.numel() != self.n_local:
+            raise GdmError("error_norms: u has %d entries, expected n_local %d" % (u_local.numel(), self.n_local))
+        if cell_errors is not None and cell_errors.numel() != self.n_owned_cells:
+            raise GdmError("error_norms: cell_errors has %d entries, expected %d" % (cell_errors.numel(),
+                                                                                     self.n_owned_cells))
+        prm = (ctypes.c_double * max(len(params), 1))(*[float(v) for v in params])
+        out = (ctypes.c_double * 3)()
+        check(self.lib.gdm_error_norms(self.h, _ptr(u_local), int(fn_kind), prm, len(params), float(t),
+                                       _ptr(cell_errors), out), "gdm_error_norms")
+        return tuple(out)
+
+    @property
+    def n_owned_cells(self):
+        n = max(0, self.layout["cell_plane_end"] - self.layout["cell_plane_begin"])
+        for d in range(self.dim - 1):
+            n *= self.mesh.n_subdivisions[d]
+        return n
+
     def dot(self, x, y):
         r = ctypes.c_double(0.0)
         check(self.lib.gdm_vec_dot(self.h, x.numel(), _ptr(x), _ptr(y), ctypes.byref(r)), "gdm_vec_dot")

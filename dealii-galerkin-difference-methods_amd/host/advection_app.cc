@@ -15,9 +15,13 @@
 // thread per rank (z-slabs of system.h:720-757, all on DEVICE), ghost planes
 // and dots through GDM::HIP::ThreadGroup (an MPI communicator's role), the
 // distributed CG mass solve; OUT holds the ranks' owned values in rank order.
+// With DEVBC the final errors against the exact solution are computed on the
+// device (AdvectionProblem::postprocess -> gdm_error_norms) and printed in the
+// reference's postprocess format (time, L2, L1, Linf).
 #include <gdm/hip/operators.h>
 #include <gdm/hip/thread_communicator.h>
 
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -47,6 +51,13 @@ double dg_dt(const GDM::HIP::Point &x, double t) {
   return s;
 }
 
+// time after `steps` steps of DiscreteTime(0, 1, dx cfl / max_val), max_val = 1
+double time_of(unsigned int steps, int n, double cfl) {
+  GDM::HIP::DiscreteTime t(0.0, 1.0, (1.0 / n) * cfl);
+  for (unsigned int i = 0; i < steps && !t.is_at_end(); ++i) t.advance_time();
+  return t.get_current_time();
+}
+
 template <int dim>
 GDM::HIP::Parameters<dim> make_params(int p, int n, double cfl, int device, int devbc) {
   GDM::HIP::Parameters<dim> params;
@@ -73,10 +84,12 @@ template <int dim>
 int run(int p, int n, int steps, double cfl, const char *out, int device, int devbc, int n_ranks) {
   std::vector<double> u;
   unsigned int done = 0;
+  std::array<double, 6> norms{{-1.0, -1.0, -1.0, 0.0, 0.0, 0.0}};
   if (n_ranks <= 1) {
     GDM::HIP::AdvectionProblem<dim> problem(make_params<dim>(p, n, cfl, device, devbc));
     done = problem.run(steps);
     u = problem.get_solution();
+    if (devbc) norms = problem.postprocess(time_of(done, n, cfl));
   } else {
     gdm_mesh_desc mesh{};
     mesh.dim = dim;
@@ -108,6 +121,10 @@ int run(int p, int n, int steps, double cfl, const char *out, int device, int de
           GDM::HIP::AdvectionProblem<dim> problem(params, &comm);
           steps_done[r] = problem.run(steps);
           parts[r] = problem.get_solution();
+          if (devbc) {
+            const std::array<double, 6> e = problem.postprocess(time_of(steps_done[r], n, cfl));
+            if (r == 0) norms = e;
+          }
         } catch (const std::exception &e) {
           errors[r] = e.what();
           std::fprintf(stderr, "rank %d: %s\n", r, e.what());
@@ -121,6 +138,8 @@ int run(int p, int n, int steps, double cfl, const char *out, int device, int de
   double s = 0.0;
   for (double v : u) s += v * v;
   std::printf("steps %u  |u|_2 %.15e\n", done, std::sqrt(s));
+  if (devbc)  // the reference's postprocess line (problem.h:427-433): counter, time, L2, L1, Linf
+    std::printf("%5d %8.5f %14.8e %14.8e %14.8e\n", 0, time_of(done, n, cfl), norms[2], norms[1], norms[0]);
   std::ofstream f(out, std::ios::binary);
   f.write(reinterpret_cast<const char *>(u.data()), sizeof(double) * u.size());
   return f.good() ? 0 : 3;

@@ -170,6 +170,8 @@ class Communicator {
   // fill the ghost planes of `local` (engine-local layout of `op`) from the slab neighbours
   virtual void update_ghost_values(gdm_op *op, DeviceVector &local) = 0;
   virtual double sum(double local_value) = 0;
+  // Utilities::MPI::max (the Linf reduction of the postprocess, problem.h:410-411)
+  virtual double max(double local_value) = 0;
 };
 
 // RK_CLASSIC_FOURTH_ORDER (deal.II TimeStepping): c_i, a_{i,i-1}, b_i
@@ -485,6 +487,29 @@ class AdvectionProblem {
     return std::vector<double>(v.begin() + o, v.begin() + o + L.n_owned);
   }
   const BlockVector &get_solution_vector() const { return solution; }
+
+  // postprocess(time, solution) (problem.h:269-485), error part on the device:
+  // {Linf, L1, L2, Linf_face, L1_face, L2_face} of u - exact_solution(time)
+  // over QGauss(p+1) on the owned cells, reduced over the ranks like the
+  // reference (max, sum, sqrt of the summed squares).  The uncut box has no
+  // immersed surface, so the face norms are 0.  The exact solution must be a
+  // built-in device function (Parameters::boundary_function).
+  std::array<double, 6> postprocess(const double time) {
+    if (params.boundary_function < 0)
+      throw Error("AdvectionProblem::postprocess: needs a built-in exact solution (boundary_function)");
+    if (params.n_ranks != 1) comm->update_ghost_values(stiffness_matrix_operator.handle(), solution.block(1));
+    double e[3];
+    check(gdm_error_norms(stiffness_matrix_operator.handle(), solution.block(1).get_values(), params.boundary_function,
+                          params.boundary_function_params.data(), (int)params.boundary_function_params.size(), time,
+                          nullptr, e),
+          "gdm_error_norms");
+    if (params.n_ranks != 1) {
+      e[0] = comm->max(e[0]);
+      e[1] = comm->sum(e[1]);
+      e[2] = std::sqrt(comm->sum(e[2] * e[2]));
+    }
+    return {{e[0], e[1], e[2], 0.0, 0.0, 0.0}};
+  }
 
  private:
   // VectorTools::interpolate of the GDM vertex basis = vertex values (vector_tools.h:11-23)

@@ -68,6 +68,14 @@ class ThreadGroup {
       g.barrier();
       return s;
     }
+    double max(double v) override {
+      g.vals[rank] = v;
+      g.barrier();
+      double s = g.vals[0];
+      for (double x : g.vals) s = x > s ? x : s;
+      g.barrier();
+      return s;
+    }
     const gdm_halo &get_plan() const { return plan; }
 
    private:

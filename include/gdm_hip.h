@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 4
+#define GDM_HIP_ABI_VERSION 5
 
 enum gdm_status {
   GDM_OK = 0,
@@ -253,6 +253,27 @@ int gdm_vec_rk_update(gdm_op *op, int64_t n, double beta, const double *k, const
                       double alpha, const double *y, double *Y);
 int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_params, double t, int derivative,
                       double *bc_values);
+
+/* ----------------------------------------------------------------------
+ * Postprocess on the device
+ *   gdm_error_norms     the volume error norms of the reference's
+ *                       postprocess (applications/advection/include/gdm/
+ *                       advection/problem.h:269-425, the uncut mesh has no
+ *                       immersed surface, so its *_face norms are 0):
+ *                       norms_host = {Linf, L1, L2} of u - f(t) over
+ *                       QGauss(p+1) on this rank's locally owned cells, f a
+ *                       built-in function (gdm_fn_kind, same params as
+ *                       gdm_eval_boundary).  u_local: engine-local vector
+ *                       (ghost planes filled).  The caller reduces across
+ *                       ranks as the reference does: Linf max, L1 sum,
+ *                       L2 = sqrt(sum L2^2) (problem.h:410-425).
+ *                       cell_errors (device, optional, n_owned_cells =
+ *                       product of the owned cell counts, lexicographic
+ *                       x fastest) = integrate_difference's per-cell L2
+ *                       errors (include/gdm/vector_tools.h:25-86).
+ * ---------------------------------------------------------------------- */
+int gdm_error_norms(gdm_op *op, const double *u_local, int fn_kind, const double *params, int n_params, double t,
+                    double *cell_errors, double *norms_host);
 
 /* memory helpers for callers without their own device allocator */
 int gdm_malloc(gdm_op *op, size_t bytes, void **ptr);

@@ -937,12 +937,15 @@ done:
 }
 
 /* ------------------------------------------------------------------------- */
-/* L2 error against cell-quadrature-point values of the exact solution         */
-/* (vector_tools.h:25-86 + compute_global_error(L2)); exact given at cell     */
-/* quadrature points, cell-major (n_cells x (p+1)^dim).                        */
+/* Error norms against cell-quadrature-point values of the exact solution      */
+/* (vector_tools.h:25-86 integrate_difference(L2) per cell + compute_global_   */
+/* error; the volume part of advection/problem.h:269-425 postprocess: Linf,    */
+/* L1, L2 over QGauss(p+1)); exact given at cell quadrature points, cell-major */
+/* (n_cells x (p+1)^dim, q lexicographic, x fastest).  out = {Linf, L1, L2};   */
+/* cell_l2 (optional) = the per-cell L2 errors of integrate_difference.        */
 /* ------------------------------------------------------------------------- */
-double gdmo_l2_error(int dim, int p, const unsigned *nsub, const double *lo, const double *hi,
-                     const double *u, const double *exact_q)
+void gdmo_error_norms(int dim, int p, const unsigned *nsub, const double *lo, const double *hi, const double *u,
+                      const double *exact_q, double *out, double *cell_l2)
 {
   tables_t T;
   build_tables(&T, dim, p);
@@ -951,7 +954,7 @@ double gdmo_l2_error(int dim, int p, const unsigned *nsub, const double *lo, con
   uint64_t *dofs = (uint64_t *)malloc(sizeof(uint64_t) * nd);
   double *sv = (double *)malloc(sizeof(double) * nd * nd);
   unsigned prev_cat[3] = {~0u, ~0u, ~0u};
-  double total = 0.0;
+  double l2 = 0.0, l1 = 0.0, linf = 0.0;
   for (unsigned c = 0; c < nc; ++c) {
     unsigned cidx[3], cat[3];
     double h[3];
@@ -979,12 +982,27 @@ double gdmo_l2_error(int dim, int p, const unsigned *nsub, const double *lo, con
         uq += u[dofs[j]] * sv[j * nd + q];
       const double e = uq - exact_q[(uint64_t)c * nd + q];
       diff += e * e * wq;
+      l1 += fabs(e) * wq;
+      if (fabs(e) > linf)
+        linf = fabs(e);
     }
-    total += diff; /* sqrt per cell then squared sum == same */
+    if (cell_l2)
+      cell_l2[c] = sqrt(diff);
+    l2 += diff; /* sqrt per cell then squared sum == same */
   }
   free(dofs);
   free(sv);
-  return sqrt(total);
+  out[0] = linf;
+  out[1] = l1;
+  out[2] = sqrt(l2);
+}
+
+double gdmo_l2_error(int dim, int p, const unsigned *nsub, const double *lo, const double *hi,
+                     const double *u, const double *exact_q)
+{
+  double out[3];
+  gdmo_error_norms(dim, p, nsub, lo, hi, u, exact_q, out, NULL);
+  return out[2];
 }
 
 /* physical coordinates of all cell quadrature points, cell-major */

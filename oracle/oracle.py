@@ -58,6 +58,7 @@ def lib():
         L.gdmo_cg.argtypes = [i64, P, P, P, P, P, i, i, d, d]
         L.gdmo_l2_error.restype = d
         L.gdmo_l2_error.argtypes = [i, i, P, P, P, P, P]
+        L.gdmo_error_norms.argtypes = [i, i, P, P, P, P, P, P, P]
         L.gdmo_cell_qpoints.argtypes = [i, i, P, P, P, P]
         L.gdmo_matrices_1d.argtypes = [i, u, d, P, P, P]
         L.gdmo_kron_apply.argtypes = [P, i, i, P, P, P]
@@ -181,6 +182,18 @@ class Mesh:
         u = np.ascontiguousarray(u, dtype=np.float64)
         e = np.ascontiguousarray(exact_q, dtype=np.float64)
         return lib().gdmo_l2_error(self.dim, self.p, _p(self.nsub), _p(self.lo), _p(self.hi), _p(u), _p(e))
+
+    def error_norms(self, u, exact_q, cells=False):
+        """(Linf, L1, L2) of u - exact over QGauss(p+1) (advection/problem.h:
+        330-425 volume part); cells=True also returns integrate_difference's
+        per-cell L2 errors (vector_tools.h:25-86)."""
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        e = np.ascontiguousarray(exact_q, dtype=np.float64)
+        out = np.zeros(3)
+        cl = np.zeros(self.n_cells) if cells else None
+        lib().gdmo_error_norms(self.dim, self.p, _p(self.nsub), _p(self.lo), _p(self.hi), _p(u), _p(e), _p(out),
+                               _p(cl) if cells else None)
+        return (tuple(out), cl) if cells else tuple(out)
 
     # -- Kronecker cross-check ---------------------------------------------
     def matrices_1d(self, d):

@@ -93,6 +93,17 @@ def test_driver_rk4_matches_oracle(tmp_path, dim, p, n, steps, devbc):
     ref = oracle_rk4(dim, p, n, steps, 0.1)
     assert u.shape == ref.shape
     assert np.linalg.norm(u - ref) / np.linalg.norm(ref) < 1e-10
+    if devbc:
+        # postprocess on the device (gdm_error_norms) vs the oracle's cell loop
+        # on the same final field; printed as the reference's "%14.8e" line
+        t, l2, l1, linf = (float(v) for v in r.stdout.strip().splitlines()[-1].split()[1:])
+        assert abs(t - steps * 0.1 / n) < 1e-12
+        m = O.Mesh(dim, p, n)
+        xq = m.cell_qpoints()
+        ex = _g([xq[:, d] for d in range(3)], t, dim)
+        ref_n = m.error_norms(u, ex)
+        for got, want in zip((linf, l1, l2), ref_n):
+            assert abs(got - want) <= 1e-7 * want
 
 
 WAVE_APP = os.path.join(ROOT, "dealii-galerkin-difference-methods_amd", "lib", "host", "wave_app")
@@ -154,10 +165,14 @@ def test_driver_multirank_matches_single_rank(tmp_path, dim, p, n, steps, n_rank
     cells' points) reproduces the single-rank run (exact Kronecker solve)."""
     out1, outn = tmp_path / "u1.bin", tmp_path / "un.bin"
     base = [APP, str(dim), str(p), str(n), str(steps), "0.1"]
-    r = subprocess.run(base + [str(out1), "0", "1", "1"], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
+    r1 = subprocess.run(base + [str(out1), "0", "1", "1"], capture_output=True, text=True, timeout=120)
+    assert r1.returncode == 0, r1.stderr
     r = subprocess.run(base + [str(outn), "0", "1", str(n_ranks)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     u1, un = np.fromfile(out1, dtype=np.float64), np.fromfile(outn, dtype=np.float64)
     assert u1.shape == un.shape
     assert np.linalg.norm(un - u1) / np.linalg.norm(u1) < 1e-10
+    # postprocess reduced over the ranks (max / sum / sqrt-sum-sq) = one rank
+    e1 = [float(v) for v in r1.stdout.strip().splitlines()[-1].split()[2:]]
+    en = [float(v) for v in r.stdout.strip().splitlines()[-1].split()[2:]]
+    np.testing.assert_allclose(en, e1, rtol=1e-7)
