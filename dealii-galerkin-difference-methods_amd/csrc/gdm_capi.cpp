@@ -81,6 +81,30 @@ struct Face {
 // shared with the sparse-matrix entry points (gdm_csr.hip)
 int gdm_internal_set_error(int code, const char *msg) { return fail(code, msg); }
 
+// line-solve tables of one banded SPD matrix (build_line_tables)
+struct LineTables {
+  double *lrow = nullptr, *invd = nullptr;               // v2 row form
+  double *l3 = nullptr, *u3 = nullptr, *d3 = nullptr;    // v3 split rows
+  std::vector<double> cst;                               // v3 interior fixed-point row
+  int row_lo = 0, row_hi = 0;
+};
+
+// Distributed exact mass inverse along the partitioned direction (truncated
+// SPIKE, gdm_mass_solve_slab / gdm_mass_solve_interface): the slab's own
+// diagonal block A_r of M_q, its spikes V = A_r^-1 B_r (coupling to the next
+// slab's first p planes) and W = A_r^-1 C_r (previous slab's last p planes),
+// and the two p x 2p rows of the interface-system inverses.
+struct SpikeTables {
+  bool built = false;
+  double eps = 0.0;        // largest dropped far-spike entry over all slabs
+  int n_planes = 0;        // owned planes of this rank
+  int has_lo = 0, has_hi = 0;
+  LineTables slab;         // A_r
+  double *VW = nullptr;    // device [n_planes][2p]: V row k | W row k
+  double *S = nullptr;     // device [2][p][2p]: lower-interface rows (x_{r-1}^bot), upper (x_{r+1}^top)
+  int k_begin = 0, k_end = 0;  // planes the correction touches
+};
+
 struct gdm_op {
   int device = 0;
   hipStream_t own_stream = nullptr, stream = nullptr;
@@ -123,6 +147,7 @@ struct gdm_op {
   int row_lo3[3] = {0, 0, 0}, row_hi3[3] = {0, 0, 0};
   std::vector<double> cst3_host[3];
   double *bc_tab = nullptr;  // gdm_eval_boundary: per-face 1D factor tables
+  SpikeTables spike;         // distributed mass inverse (n_ranks > 1)
   // gdm_error_norms: shape values per category, per-workgroup partials, result
   double *err_S = nullptr, *err_partial = nullptr;
   static constexpr int n_err_partial = 1024;
@@ -232,6 +257,58 @@ gdm::Band identity_band(int p) {
   gdm::Band b(1, p);
   b(0, 0) = 1.0;
   return b;
+}
+
+// Line-solve tables of one SPD band matrix M = L L^T (gdm_mass.hip): the v2
+// row form (lrow / invd, zero-padded for the backward sweep) and, where the v3
+// single-sweep kernel exists for p, its split rows prescaled by 1 / L_ii,
+// zero-padded by 3C + p rows, plus the run of rows around the middle that equal
+// the middle row bitwise (the interior fixed point of the factorisation).
+LineTables build_line_tables(gdm_op *op, const gdm::Band &M) {
+  const int p = op->p;
+  LineTables t;
+  std::vector<double> lrow, invd;
+  gdm::cholesky_band(M, lrow, invd);
+  std::vector<double> lrow_pad = lrow;
+  lrow_pad.resize(lrow.size() + (size_t)p * (p + 1), 0.0);  // zero pad for the backward sweep
+  t.lrow = keep(op, dev_upload(lrow_pad));
+  t.invd = keep(op, dev_upload(invd));
+  const int C3 = gdmk_mass3_chunk(p);
+  if (C3 > 0) {
+    const int n = M.n, rows = n + 3 * C3 + p;
+    const int wl = p + 1;
+    std::vector<double> l3((size_t)rows * p, 0.0), u3((size_t)rows * p, 0.0), d3((size_t)rows, 0.0);
+    for (int i = 0; i < n; ++i) {
+      for (int k = 0; k < p; ++k) l3[(size_t)i * p + k] = lrow[(size_t)i * wl + k] * invd[i];
+      for (int m = 1; m <= p; ++m)
+        if (i + m < n) u3[(size_t)i * p + m - 1] = lrow[(size_t)(i + m) * wl + (p - m)] * invd[i];
+      d3[i] = invd[i];
+    }
+    const int mid = n / 2;
+    auto same = [&](int i) {
+      if (d3[i] != d3[mid]) return false;
+      for (int k = 0; k < p; ++k)
+        if (l3[(size_t)i * p + k] != l3[(size_t)mid * p + k] || u3[(size_t)i * p + k] != u3[(size_t)mid * p + k])
+          return false;
+      return true;
+    };
+    int lo = mid, hi = mid + 1;
+    while (lo > 0 && same(lo - 1)) --lo;
+    while (hi < n && same(hi)) ++hi;
+    std::vector<double> cst(2 * p + 1);
+    for (int k = 0; k < p; ++k) {
+      cst[k] = l3[(size_t)mid * p + k];
+      cst[p + k] = u3[(size_t)mid * p + k];
+    }
+    cst[2 * p] = d3[mid];
+    t.l3 = keep(op, dev_upload(l3));
+    t.u3 = keep(op, dev_upload(u3));
+    t.d3 = keep(op, dev_upload(d3));
+    t.cst = cst;
+    t.row_lo = lo;
+    t.row_hi = hi;
+  }
+  return t;
 }
 
 void build_tables(gdm_op *op) {
@@ -410,49 +487,15 @@ void build_tables(gdm_op *op) {
   // banded Cholesky factors of the 1D mass matrices (exact Kronecker inverse)
   for (int ax = 0; ax < 3; ++ax) {
     if (op->K[ax] <= 1) continue;
-    std::vector<double> lrow, invd;
-    gdm::cholesky_band(M[ax], lrow, invd);
-    lrow.resize(lrow.size() + (size_t)p * (p + 1), 0.0);  // zero pad for the backward sweep
-    op->lrow[ax] = keep(op, dev_upload(lrow));
-    op->invd[ax] = keep(op, dev_upload(invd));
-    // v3: split rows, zero-padded by 3C + p rows past the line end
-    const int C3 = gdmk_mass3_chunk(p);
-    if (C3 > 0) {
-      const int n = M[ax].n, rows = n + 3 * C3 + p;
-      const int wl = p + 1;
-      std::vector<double> l3((size_t)rows * p, 0.0), u3((size_t)rows * p, 0.0), d3((size_t)rows, 0.0);
-      for (int i = 0; i < n; ++i) {
-        for (int k = 0; k < p; ++k) l3[(size_t)i * p + k] = lrow[(size_t)i * wl + k] * invd[i];
-        for (int m = 1; m <= p; ++m)
-          if (i + m < n) u3[(size_t)i * p + m - 1] = lrow[(size_t)(i + m) * wl + (p - m)] * invd[i];
-        d3[i] = invd[i];
-      }
-      // the run of rows around the middle that equal the middle row bitwise
-      const int mid = n / 2;
-      auto same = [&](int i) {
-        if (d3[i] != d3[mid]) return false;
-        for (int k = 0; k < p; ++k)
-          if (l3[(size_t)i * p + k] != l3[(size_t)mid * p + k] || u3[(size_t)i * p + k] != u3[(size_t)mid * p + k])
-            return false;
-        return true;
-      };
-      int lo = mid, hi = mid + 1;
-      while (lo > 0 && same(lo - 1)) --lo;
-      while (hi < n && same(hi)) ++hi;
-      std::vector<double> cst(2 * p + 1);
-      for (int k = 0; k < p; ++k) {
-        cst[k] = l3[(size_t)mid * p + k];
-        cst[p + k] = u3[(size_t)mid * p + k];
-      }
-      cst[2 * p] = d3[mid];
-      op->l3[ax] = keep(op, dev_upload(l3));
-      op->u3[ax] = keep(op, dev_upload(u3));
-      op->d3[ax] = keep(op, dev_upload(d3));
-      op->cst3[ax] = keep(op, dev_upload(cst));  // device copy unused by the kernels; host copy below
-      op->cst3_host[ax] = cst;
-      op->row_lo3[ax] = lo;
-      op->row_hi3[ax] = hi;
-    }
+    LineTables t = build_line_tables(op, M[ax]);
+    op->lrow[ax] = t.lrow;
+    op->invd[ax] = t.invd;
+    op->l3[ax] = t.l3;
+    op->u3[ax] = t.u3;
+    op->d3[ax] = t.d3;
+    op->cst3_host[ax] = t.cst;
+    op->row_lo3[ax] = t.row_lo;
+    op->row_hi3[ax] = t.row_hi;
   }
 }
 
@@ -795,6 +838,219 @@ int choose_zchunk(const gdm_op *op) {
 
 }  // namespace
 
+namespace {
+
+constexpr double kSpikeTol = 1e-15;
+
+// x = M^-1 b with the row-form banded Cholesky factor of gdm::cholesky_band
+void band_chol_solve(const std::vector<double> &lrow, const std::vector<double> &invd, int n, int hb, double *b) {
+  const int wl = hb + 1;
+  for (int i = 0; i < n; ++i) {
+    double s = b[i];
+    for (int k = 0; k < hb; ++k) {
+      const int j = i - hb + k;
+      if (j >= 0) s -= lrow[(size_t)i * wl + k] * b[j];
+    }
+    b[i] = s * invd[i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double s = b[i];
+    for (int m = 1; m <= hb && i + m < n; ++m) s -= lrow[(size_t)(i + m) * wl + (hb - m)] * b[i + m];
+    b[i] = s * invd[i];
+  }
+}
+
+// diagonal block of M on planes [pb, pe) and its spikes:
+// V[k][j] = (A^-1 M[pb:pe, pe + j])_k, W[k][j] = (A^-1 M[pb:pe, pb - p + j])_k
+struct SlabSpikes {
+  gdm::Band A;
+  std::vector<double> V, W;
+};
+SlabSpikes slab_spikes(const gdm::Band &M, int p, int pb, int pe) {
+  const int n = pe - pb;
+  SlabSpikes r;
+  r.A = gdm::Band(n, p);
+  for (int i = 0; i < n; ++i)
+    for (int j = std::max(0, i - p); j <= std::min(n - 1, i + p); ++j) r.A(i, j) = M(pb + i, pb + j);
+  std::vector<double> lrow, invd, col(n);
+  gdm::cholesky_band(r.A, lrow, invd);
+  r.V.assign((size_t)n * p, 0.0);
+  r.W.assign((size_t)n * p, 0.0);
+  for (int j = 0; j < p; ++j) {
+    for (int i = 0; i < n; ++i) col[i] = M(pb + i, pe + j);
+    band_chol_solve(lrow, invd, n, p, col.data());
+    for (int i = 0; i < n; ++i) r.V[(size_t)i * p + j] = col[i];
+    for (int i = 0; i < n; ++i) col[i] = M(pb + i, pb - p + j);
+    band_chol_solve(lrow, invd, n, p, col.data());
+    for (int i = 0; i < n; ++i) r.W[(size_t)i * p + j] = col[i];
+  }
+  return r;
+}
+
+// Rows [r0, r0 + p) of the inverse of the interface system
+// [[I, Vb], [Wt, I]] (2p x 2p) by Gauss-Jordan with partial pivoting.
+std::vector<double> interface_rows(const std::vector<double> &Vb, const std::vector<double> &Wt, int p, int r0) {
+  const int m = 2 * p;
+  std::vector<double> a((size_t)m * 2 * m, 0.0);
+  for (int i = 0; i < m; ++i) {
+    a[(size_t)i * 2 * m + i] = 1.0;
+    a[(size_t)i * 2 * m + m + i] = 1.0;
+  }
+  for (int i = 0; i < p; ++i)
+    for (int j = 0; j < p; ++j) {
+      a[(size_t)i * 2 * m + p + j] = Vb[(size_t)i * p + j];
+      a[(size_t)(p + i) * 2 * m + j] = Wt[(size_t)i * p + j];
+    }
+  for (int c = 0; c < m; ++c) {
+    int piv = c;
+    for (int i = c + 1; i < m; ++i)
+      if (std::abs(a[(size_t)i * 2 * m + c]) > std::abs(a[(size_t)piv * 2 * m + c])) piv = i;
+    if (piv != c)
+      for (int k = 0; k < 2 * m; ++k) std::swap(a[(size_t)c * 2 * m + k], a[(size_t)piv * 2 * m + k]);
+    const double d = a[(size_t)c * 2 * m + c];
+    if (d == 0.0) throw std::runtime_error("singular interface system");
+    for (int k = 0; k < 2 * m; ++k) a[(size_t)c * 2 * m + k] /= d;
+    for (int i = 0; i < m; ++i) {
+      if (i == c) continue;
+      const double f = a[(size_t)i * 2 * m + c];
+      if (f != 0.0)
+        for (int k = 0; k < 2 * m; ++k) a[(size_t)i * 2 * m + k] -= f * a[(size_t)c * 2 * m + k];
+    }
+  }
+  std::vector<double> out((size_t)p * m);
+  for (int i = 0; i < p; ++i)
+    for (int k = 0; k < m; ++k) out[(size_t)i * m + k] = a[(size_t)(r0 + i) * 2 * m + m + k];
+  return out;
+}
+
+// Largest entry of the couplings the truncated interface systems drop: the
+// far spikes W_s^bot (slab s's last p rows of W) and V_s^top over all slabs.
+double spike_eps(const gdm::Band &M, int p, unsigned n_cells, unsigned n_ranks) {
+  double eps = 0.0;
+  for (unsigned s = 0; s < n_ranks; ++s) {
+    const gdm::Slab sl = gdm::slab_partition(n_cells, n_ranks, s);
+    const int pb = (int)sl.plane_begin, pe = (int)std::max(sl.plane_begin, sl.plane_end), n = pe - pb;
+    if (n_ranks == 1) return 0.0;
+    if (n < p) return 1.0;  // a slab thinner than the interface
+    const SlabSpikes sp = slab_spikes(M, p, pb, pe);
+    for (int a = 0; a < p; ++a)
+      for (int j = 0; j < p; ++j) {
+        if (s > 0) eps = std::max(eps, std::abs(sp.W[(size_t)(n - p + a) * p + j]));
+        if (s + 1 < n_ranks) eps = std::max(eps, std::abs(sp.V[(size_t)a * p + j]));
+      }
+  }
+  return eps;
+}
+
+void build_spike(gdm_op *op) {
+  SpikeTables &T = op->spike;
+  const int p = op->p, q = op->dim - 1;
+  const unsigned nc = (unsigned)op->mesh.n_subdivisions[q], R = (unsigned)op->mesh.n_ranks, r = (unsigned)op->mesh.rank;
+  const gdm::Band M = gdm::assemble_1d(p, nc, (op->mesh.hi[q] - op->mesh.lo[q]) / nc).M;
+  T.built = true;
+  T.eps = spike_eps(M, p, nc, R);
+  if (T.eps > kSpikeTol) return;
+  auto planes = [&](unsigned s) {
+    const gdm::Slab sl = gdm::slab_partition(nc, R, s);
+    return std::make_pair((int)sl.plane_begin, (int)std::max(sl.plane_begin, sl.plane_end));
+  };
+  const auto [pb, pe] = planes(r);
+  const int n = pe - pb;
+  T.n_planes = n;
+  T.has_lo = r > 0;
+  T.has_hi = r + 1 < R;
+  const gdm_layout &L = op->layout;
+  if ((T.has_lo && L.ghost_planes_below != p) || (T.has_hi && L.ghost_planes_above != p))
+    throw std::runtime_error("spike: ghost layer shallower than p planes");
+  const SlabSpikes me = slab_spikes(M, p, pb, pe);
+  T.slab = build_line_tables(op, me.A);
+  std::vector<double> VW((size_t)n * 2 * p), S((size_t)2 * p * 2 * p, 0.0);
+  for (int k = 0; k < n; ++k)
+    for (int j = 0; j < p; ++j) {
+      VW[(size_t)k * 2 * p + j] = T.has_hi ? me.V[(size_t)k * p + j] : 0.0;
+      VW[(size_t)k * 2 * p + p + j] = T.has_lo ? me.W[(size_t)k * p + j] : 0.0;
+    }
+  auto rows = [&](const std::vector<double> &X, int first) {
+    return std::vector<double>(X.begin() + (size_t)first * p, X.begin() + (size_t)(first + p) * p);
+  };
+  if (T.has_lo) {  // interface (r-1, r): x_{r-1}^bot = rows [0, p)
+    const auto [qb, qe] = planes(r - 1);
+    const SlabSpikes lo = slab_spikes(M, p, qb, qe);
+    const std::vector<double> X = interface_rows(rows(lo.V, qe - qb - p), rows(me.W, 0), p, 0);
+    std::copy(X.begin(), X.end(), S.begin());
+  }
+  if (T.has_hi) {  // interface (r, r+1): x_{r+1}^top = rows [p, 2p)
+    const auto [qb, qe] = planes(r + 1);
+    const SlabSpikes hi = slab_spikes(M, p, qb, qe);
+    const std::vector<double> X = interface_rows(rows(me.V, n - p), rows(hi.W, 0), p, p);
+    std::copy(X.begin(), X.end(), S.begin() + (size_t)p * 2 * p);
+  }
+  // planes whose correction can change x (spike rows above 1e-18)
+  T.k_begin = n;
+  T.k_end = 0;
+  for (int k = 0; k < n; ++k) {
+    double mx = 0.0;
+    for (int j = 0; j < 2 * p; ++j) mx = std::max(mx, std::abs(VW[(size_t)k * 2 * p + j]));
+    if (mx > 1e-18) {
+      T.k_begin = std::min(T.k_begin, k);
+      T.k_end = k + 1;
+    }
+  }
+  T.VW = keep(op, dev_upload(VW));
+  T.S = keep(op, dev_upload(S));
+}
+
+// the line solves of M^-1 along every kernel axis; `part` replaces the
+// partitioned axis' tables by the slab's diagonal block (multi-rank)
+void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, const LineTables *part) {
+  const int64_t n = op->layout.n_owned;
+  if (n <= 0) return;
+  int64_t K[3] = {op->K[0], op->K[1], op->K[2]};
+  LineTables tab[3];
+  for (int ax = 0; ax < 3; ++ax) {
+    tab[ax].lrow = op->lrow[ax];
+    tab[ax].invd = op->invd[ax];
+    tab[ax].l3 = op->l3[ax];
+    tab[ax].u3 = op->u3[ax];
+    tab[ax].d3 = op->d3[ax];
+    tab[ax].cst = op->cst3_host[ax];
+    tab[ax].row_lo = op->row_lo3[ax];
+    tab[ax].row_hi = op->row_hi3[ax];
+  }
+  if (part) {
+    tab[op->part_axis] = *part;
+    K[op->part_axis] = op->layout.owned_plane_end - op->layout.owned_plane_begin;
+  }
+  const int64_t X = K[0], Y = K[1], Z = K[2];
+  // v3 (gdm_mass.hip, single sweep per direction) where supported, else v2
+  // (two sweeps); the first pass reads rhs and writes x, later passes in place
+  const double *in = rhs_owned;
+  const int wg = op->mass_max_wgs;
+  const bool v3 = op->mass_version >= 3 && gdmk_mass3_chunk(op->p) > 0;
+  auto pass = [&](int ax, int dir_kind, int64_t len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,
+                  const char *what) {
+    const LineTables &t = tab[ax];
+    const bool aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(x_owned)) & 15) == 0;
+    if (v3 && t.l3 && (dir_kind == 1 || (len % 2 == 0 && aligned)))
+      hip_check(gdmk_launch_mass3(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, t.l3, t.u3, t.d3,
+                                  t.cst.data(), t.row_lo, t.row_hi, op->stream),
+                what);
+    else
+      hip_check(gdmk_launch_mass_lines(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, t.lrow, t.invd,
+                                       wg, op->stream),
+                what);
+    in = x_owned;
+  };
+  const bool part_z = part && op->part_axis == 2, part_y = part && op->part_axis == 1;
+  if (Z > 1 || part_z) pass(2, 1, Z, X * Y, X * Y, X * Y, 0, "mass z");   // z lines: (x, y) -> base = l, step X*Y
+  if (Y > 1 || part_y) pass(1, 1, Y, X, X * Z, X, X * Y, "mass y");       // y lines: (x, z) -> base = z*X*Y + x, step X
+  if (X > 1) pass(0, 0, X, 1, Y * Z, 1, 0, "mass x");                     // x lines: contiguous rows of length X
+  if (in != x_owned)
+    hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+}
+
+}  // namespace
+
 extern "C" {
 
 int gdm_last_error(char *buf, size_t len) {
@@ -1104,7 +1360,8 @@ int gdm_mass_apply(gdm_op *op, const double *src_local, double *dst_owned) {
 int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   if (op->mesh.n_ranks != 1)
-    return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve: the exact Kronecker inverse is single-rank in this version");
+    return fail(GDM_ERR_UNSUPPORTED,
+                "gdm_mass_solve: single rank; multi-rank: gdm_mass_solve_slab + ghost exchange + gdm_mass_solve_interface");
   if (op->mesh.periodic)
     return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve: periodic constraints couple the line ends; use gdm_mass_solve_cg");
   if (!rhs_owned || !x_owned) return fail(GDM_ERR_ARG, "NULL vector");
@@ -1127,30 +1384,62 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
                                        op->stream), "chol x");
     return GDM_OK;
   }
-  // v3 (gdm_mass.hip, single sweep per direction) where supported, else v2
-  // (two sweeps); the first pass reads rhs and writes x, later passes in place
-  const double *in = rhs_owned;
-  const int wg = op->mass_max_wgs;
-  const bool v3 = op->mass_version >= 3 && gdmk_mass3_chunk(op->p) > 0;
-  auto pass = [&](int ax, int dir_kind, int64_t len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,
-                  const char *what) {
-    const bool aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(x_owned)) & 15) == 0;
-    if (v3 && op->l3[ax] && (dir_kind == 1 || (len % 2 == 0 && aligned)))
-      hip_check(gdmk_launch_mass3(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, op->l3[ax],
-                                  op->u3[ax], op->d3[ax], op->cst3_host[ax].data(), op->row_lo3[ax], op->row_hi3[ax],
-                                  op->stream),
-                what);
-    else
-      hip_check(gdmk_launch_mass_lines(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, op->lrow[ax],
-                                       op->invd[ax], wg, op->stream),
-                what);
-    in = x_owned;
-  };
-  if (Z > 1) pass(2, 1, Z, X * Y, X * Y, X * Y, 0, "mass z");   // z lines: (x, y) -> base = l, step X*Y
-  if (Y > 1) pass(1, 1, Y, X, X * Z, X, X * Y, "mass y");       // y lines: (x, z) -> base = z*X*Y + x, step X
-  if (X > 1) pass(0, 0, X, 1, Y * Z, 1, 0, "mass x");           // x lines: contiguous rows of length X
-  if (in != x_owned)
-    hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+  mass_solve_passes(op, rhs_owned, x_owned, nullptr);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_mass_spike_eps(const gdm_mesh_desc *mesh, double *eps_host) {
+  if (!mesh || !eps_host) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  if (mesh->dim < 1 || mesh->dim > 3 || mesh->fe_degree < 1 || mesh->n_ranks < 1)
+    return fail(GDM_ERR_ARG, "bad mesh description");
+  const int q = mesh->dim - 1;
+  const unsigned nc = (unsigned)mesh->n_subdivisions[q];
+  const gdm::Band M = gdm::assemble_1d(mesh->fe_degree, nc, (mesh->hi[q] - mesh->lo[q]) / nc).M;
+  *eps_host = spike_eps(M, mesh->fe_degree, nc, (unsigned)mesh->n_ranks);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->mesh.periodic) return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_slab: periodic mesh");
+  if (op->layout.n_owned > 0 && (!rhs_owned || !x_owned)) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  if (op->mesh.n_ranks == 1) {
+    mass_solve_passes(op, rhs_owned, x_owned, nullptr);
+    return GDM_OK;
+  }
+  if (!op->spike.built) build_spike(op);
+  if (op->spike.eps > kSpikeTol) {
+    char msg[256];
+    std::snprintf(msg, sizeof msg,
+                  "gdm_mass_solve_slab: slabs too thin for the truncated interface system (dropped coupling %.3g > "
+                  "%.1g); use gdm_mass_solve_cg or fewer ranks",
+                  op->spike.eps, kSpikeTol);
+    return fail(GDM_ERR_UNSUPPORTED, msg);
+  }
+  mass_solve_passes(op, rhs_owned, x_owned, &op->spike.slab);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_mass_solve_interface(gdm_op *op, double *x_local) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->mesh.n_ranks == 1) return GDM_OK;
+  if (!op->spike.built || op->spike.eps > kSpikeTol)
+    return fail(GDM_ERR_STATE, "gdm_mass_solve_interface: call gdm_mass_solve_slab first");
+  if (op->layout.n_owned > 0 && !x_local) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  const SpikeTables &S = op->spike;
+  if (S.k_end > S.k_begin && (S.has_lo || S.has_hi))
+    hip_check(gdmk_launch_spike(op->p, x_local, op->layout.plane_size,
+                                (int64_t)op->layout.ghost_planes_below * op->layout.plane_size, S.n_planes, S.has_lo,
+                                S.has_hi, S.VW, S.S, S.k_begin, S.k_end, op->stream),
+              "spike");
   return GDM_OK;
   GDM_GUARD_END
 }

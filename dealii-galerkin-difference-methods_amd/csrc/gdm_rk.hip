@@ -154,7 +154,87 @@ __global__ void __launch_bounds__(256) vmul_kernel(int64_t n, const double *__re
     y[i] = w[i] * x[i];
 }
 
+// Interface correction of the distributed mass inverse (truncated SPIKE, see
+// gdm_capi.cpp build_spike): one thread per line of the plane, the 2p
+// interface unknowns of both slab edges in registers, then a rank-2p update
+// of the line's planes.  The edge planes are read before any plane is written
+// (one thread owns its line), so the update is in place.
+template <int P>
+__global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps, int64_t own_off, int n, int has_lo,
+                                                    int has_hi, const double *__restrict__ VW,
+                                                    const double *__restrict__ S, int k_begin, int k_end) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ps; i += (int64_t)gridDim.x * blockDim.x) {
+    double *xo = x_local + own_off + i;
+    double b[P], t[P], in[2 * P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) b[j] = t[j] = 0.0;
+    if (has_lo) {
+#pragma unroll
+      for (int a = 0; a < P; ++a) {
+        in[a] = xo[(int64_t)(a - P) * ps];
+        in[P + a] = xo[(int64_t)a * ps];
+      }
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < 2 * P; ++c) s = fma(S[j * 2 * P + c], in[c], s);
+        b[j] = s;
+      }
+    }
+    if (has_hi) {
+#pragma unroll
+      for (int a = 0; a < P; ++a) {
+        in[a] = xo[(int64_t)(n - P + a) * ps];
+        in[P + a] = xo[(int64_t)(n + a) * ps];
+      }
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < 2 * P; ++c) s = fma(S[2 * P * P + j * 2 * P + c], in[c], s);
+        t[j] = s;
+      }
+    }
+    for (int k = k_begin; k < k_end; ++k) {
+      const double *vw = VW + (size_t)k * 2 * P;
+      double c = 0.0;
+#pragma unroll
+      for (int j = 0; j < P; ++j) c = fma(vw[j], t[j], c);
+#pragma unroll
+      for (int j = 0; j < P; ++j) c = fma(vw[P + j], b[j], c);
+      xo[(int64_t)k * ps] -= c;
+    }
+  }
+}
+
 }  // namespace gdmk
+
+extern "C" hipError_t gdmk_launch_spike(int p, double *x_local, int64_t ps, int64_t own_off, int n, int has_lo,
+                                       int has_hi, const double *VW, const double *S, int k_begin, int k_end,
+                                       hipStream_t st) {
+  if (ps <= 0 || k_end <= k_begin) return hipSuccess;
+  const unsigned blocks = (unsigned)std::min<int64_t>((ps + 255) / 256, 4096);
+#define GDM_SPIKE(PP)                                                                                           \
+  case PP:                                                                                                      \
+    hipLaunchKernelGGL(gdmk::spike_kernel<PP>, dim3(blocks), dim3(256), 0, st, x_local, ps, own_off, n, has_lo, \
+                       has_hi, VW, S, k_begin, k_end);                                                          \
+    break;
+  switch (p) {
+    GDM_SPIKE(1)
+    GDM_SPIKE(2)
+    GDM_SPIKE(3)
+    GDM_SPIKE(4)
+    GDM_SPIKE(5)
+    GDM_SPIKE(6)
+    GDM_SPIKE(7)
+    GDM_SPIKE(8)
+    GDM_SPIKE(9)
+    default: return hipErrorInvalidValue;
+  }
+#undef GDM_SPIKE
+  return hipGetLastError();
+}
 
 extern "C" hipError_t gdmk_launch_rk_update(int64_t n, double beta, const double *k, const double *acc_in,
                                            double *acc_out, double alpha, const double *y, double *Y,

@@ -115,6 +115,9 @@ def load():
         "gdm_vec_rk_update": [P, i64, d, P, P, P, d, P, P],
         "gdm_eval_boundary": [P, i32, P, i32, d, i32, P],
         "gdm_error_norms": [P, P, i32, P, i32, d, P, P],
+        "gdm_mass_spike_eps": [P, P],
+        "gdm_mass_solve_slab": [P, P, P],
+        "gdm_mass_solve_interface": [P, P],
         "gdm_synchronize": [P],
         "gdm_malloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
         "gdm_free": [P, P],
@@ -164,3 +167,24 @@ def device_count():
     n = ctypes.c_int(0)
     rc = load().gdm_get_device_count(ctypes.byref(n))
     return n.value if rc == GDM_OK else 0
+
+
+def mesh_desc(dim, fe_degree, n_subdivisions, lo=0.0, hi=1.0, n_ranks=1, rank=0, periodic=0):
+    m = MeshDesc()
+    m.dim, m.fe_degree = dim, fe_degree
+    ns = list(n_subdivisions) if hasattr(n_subdivisions, "__len__") else [n_subdivisions] * dim
+    for d in range(3):
+        m.n_subdivisions[d] = int(ns[d]) if d < dim else 1
+        m.lo[d] = float(lo) if d < dim else 0.0
+        m.hi[d] = float(hi) if d < dim else 1.0
+    m.n_ranks, m.rank, m.periodic = n_ranks, rank, periodic
+    return m
+
+
+def mass_spike_eps(dim, fe_degree, n_subdivisions, n_ranks, lo=0.0, hi=1.0):
+    """Largest coupling the distributed mass inverse's truncated interface
+    systems drop (pure host, no GPU); the solve needs <= 1e-15."""
+    e = ctypes.c_double(0.0)
+    m = mesh_desc(dim, fe_degree, n_subdivisions, lo, hi, n_ranks)
+    check(load().gdm_mass_spike_eps(ctypes.byref(m), ctypes.byref(e)), "gdm_mass_spike_eps")
+    return e.value

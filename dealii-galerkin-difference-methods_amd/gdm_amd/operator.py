@@ -192,6 +192,23 @@ class GdmOperator:
                                          _ptr(out)), "gdm_eval_boundary")
         return out
 
+    def mass_solve_slab(self, rhs_owned, x_owned):
+        """Distributed exact mass inverse, step 1: the slab-local solve
+        (gdm_mass_solve_slab).  Then exchange the ghost planes of the local
+        vector holding x_owned and call mass_solve_interface."""
+        check(self.lib.gdm_mass_solve_slab(self.h, _ptr(rhs_owned), _ptr(x_owned)), "gdm_mass_solve_slab")
+        return x_owned
+
+    def mass_solve_interface(self, x_local):
+        """Distributed exact mass inverse, step 2 (gdm_mass_solve_interface):
+        the owned part of x_local (ghost planes = the neighbours' slab solves)
+        becomes M^-1 rhs."""
+        if x_local.numel() != self.n_local:
+            raise GdmError("mass_solve_interface: x has %d entries, expected n_local %d" % (x_local.numel(),
+                                                                                          self.n_local))
+        check(self.lib.gdm_mass_solve_interface(self.h, _ptr(x_local)), "gdm_mass_solve_interface")
+        return x_local
+
     def error_norms(self, u_local, fn_kind, params, t, cell_errors=None):
         """(Linf, L1, L2) of u - f(t) over QGauss(p+1) on the owned cells
         (advection/problem.h:269-425 postprocess, volume part); cell_errors

@@ -185,6 +185,26 @@ int gdm_mass_apply(gdm_op *op, const double *src_local, double *dst_owned);
  * periodic constraints: gdm_mass_solve_cg) */
 int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned);
 
+/* Distributed exact mass inverse (n_ranks > 1; replaces the CG + ILU/AMG
+ * solve of advection/problem.h:236-267 / wave/problem.h:457-502 across MPI
+ * ranks).  M^-1 = M_q^-1 (x) ... (x) M_0^-1; the in-slab directions are
+ * solved locally; the partitioned direction q = dim - 1 by a truncated SPIKE
+ * scheme: each slab solves with its own diagonal block A_r of M_q, the ranks
+ * exchange p planes with each slab neighbour (exactly the ghost planes of the
+ * stencil's update_ghost_values), and a 2p x 2p interface system per slab
+ * boundary (the same for every line) corrects the slab:
+ *   gdm_mass_solve_slab(op, rhs_owned, x_owned)   x = (A_r^-1 (x) M_y^-1 (x) M_x^-1) rhs
+ *   <copy x_owned into the owned part of a local vector; ghost exchange>
+ *   gdm_mass_solve_interface(op, x_local)          owned part of x_local = M^-1 rhs
+ * Exact up to the dropped coupling of the far spikes, which decays
+ * geometrically with the slab thickness: gdm_mass_spike_eps (pure host)
+ * reports it; the solve refuses (GDM_ERR_UNSUPPORTED) when it exceeds 1e-15
+ * (e.g. slabs thinner than ~48 planes at p = 5).  n_ranks == 1: the slab solve
+ * is gdm_mass_solve and the interface call a no-op. */
+int gdm_mass_spike_eps(const gdm_mesh_desc *mesh, double *eps_host);
+int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned);
+int gdm_mass_solve_interface(gdm_op *op, double *x_local);
+
 /* x_owned = M^-1 rhs_owned by SolverCG on the matrix-free mass operator with
  * ReductionControl(max_it, abs_tol, rel_tol) semantics, the solve of
  * prototypes/advection_01_gdm.cc:208-217 (PreconditionJacobi, rel 1e-8) and of

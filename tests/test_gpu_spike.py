@@ -1,0 +1,74 @@
+"""Distributed exact mass inverse on the device (gdm_mass_solve_slab +
+ghost exchange + gdm_mass_solve_interface, include/gdm_hip.h), all ranks of
+the partition as operators in one process, the exchange done by copying the
+neighbours' edge planes (what HaloExchange / MPI do between processes).
+
+Reference: the one-rank exact Kronecker inverse gdm_mass_solve, itself pinned
+to CG(1e-14) on the oracle's assembled mass matrix (test_gpu_parity.py) --
+the reference's *Problem::solve (advection/problem.h:236-267).
+Tolerance: rel-L2 <= 1e-13 (the truncated interface coupling is < 1e-15)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _ranks(gdm_amd, dim, p, n, R):
+    ops = [gdm_amd.GdmOperator(dim, p, n, 0.0, 1.0, "mass", n_ranks=R, rank=r) for r in range(R)]
+    return ops
+
+
+def _exchange(ops, xs):
+    """fill ghost planes of every local vector from the neighbours' owned planes"""
+    for r, op in enumerate(ops):
+        L, ps = op.layout, op.layout["plane_size"]
+        gb, ga = L["ghost_planes_below"], L["ghost_planes_above"]
+        own = L["n_owned"] // ps
+        if r > 0 and gb:
+            Ln = ops[r - 1].layout
+            e = (Ln["ghost_planes_below"] + Ln["n_owned"] // ps) * ps
+            xs[r][:gb * ps] = xs[r - 1][e - gb * ps:e]
+        if r + 1 < len(ops) and ga:
+            Ln = ops[r + 1].layout
+            b = Ln["ghost_planes_below"] * ps
+            xs[r][(gb + own) * ps:(gb + own + ga) * ps] = xs[r + 1][b:b + ga * ps]
+
+
+@pytest.mark.parametrize("dim,p,n,R", [(3, 5, (12, 10, 130), 2), (3, 5, (9, 8, 200), 3), (2, 3, (20, 150), 3),
+                                       (1, 5, 400, 4), (3, 7, (8, 9, 240), 2), (2, 9, (12, 260), 2),
+                                       (3, 1, (6, 5, 120), 4)])
+def test_slab_mass_solve_matches_single_rank(dim, p, n, R):
+    import gdm_amd
+
+    one = gdm_amd.GdmOperator(dim, p, n, 0.0, 1.0, "mass")
+    N = one.n_owned
+    r = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, N)).cuda()
+    ref = one.new_vector(False)
+    one.mass_solve(r, ref)
+    ops = _ranks(gdm_amd, dim, p, n, R)
+    xs = []
+    for op in ops:
+        L = op.layout
+        a = L["owned_plane_begin"] * L["plane_size"]
+        x = op.new_vector(True)
+        op.mass_solve_slab(r[a:a + op.n_owned].contiguous(), op.owned_view(x))
+        xs.append(x)
+    torch.cuda.synchronize()
+    _exchange(ops, xs)
+    for op, x in zip(ops, xs):
+        op.mass_solve_interface(x)
+    got = torch.cat([op.owned_view(x) for op, x in zip(ops, xs)])
+    assert float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)) < 1e-13
+
+
+def test_slab_mass_solve_refuses_thin_slabs():
+    """C4 on 8 ranks (32 planes at p = 7): the dropped coupling exceeds 1e-15,
+    the slab solve refuses instead of returning an approximate inverse."""
+    import gdm_amd
+
+    assert gdm_amd._capi.mass_spike_eps(3, 7, 255, 8) > 1e-15
+    op = gdm_amd.GdmOperator(3, 7, (8, 8, 255), 0.0, 1.0, "mass", n_ranks=8, rank=3)
+    x = op.new_vector(False)
+    with pytest.raises(gdm_amd.GdmError, match="too thin"):
+        op.mass_solve_slab(x, x)

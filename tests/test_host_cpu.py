@@ -292,3 +292,137 @@ def test_halo_plan_matches_exchange(dim, p, n_sub, n_ranks):
             planes |= {int(g) // plane for g in m.cell_dofs(idx)}
         assert h["dealii_ghost_planes_below"] == len([q for q in planes if q < pb])
         assert h["dealii_ghost_planes_above"] == len([q for q in planes if q >= pe])
+
+
+class _NpSpikeOp:
+    """numpy restatement of the distributed mass inverse's two steps (the
+    truncated SPIKE scheme of gdm_mass_solve_slab / gdm_mass_solve_interface,
+    include/gdm_hip.h) on dense 1D mass matrices -- a test double for the
+    device operator, so the exchange orchestration of
+    gdm_amd.distributed.SlabMassSolve runs on gloo without a GPU."""
+
+    def __init__(self, dim, p, n, world, rank):
+        from gdm_amd.distributed import layout, slab
+
+        m = O.Mesh(dim, p, list(n))
+        self.Ms = [_dense_1d(m, d) for d in range(dim)]
+        self.dim, self.p = dim, p
+        self.plane = int(np.prod([n[d] + 1 for d in range(dim - 1)])) if dim > 1 else 1
+        self.L = layout(n[dim - 1], world, rank, self.plane, p)
+        self.slabs = [slab(n[dim - 1], world, s)[:2] for s in range(world)]
+        self.rank, self.world = rank, world
+
+    def owned_view(self, local):
+        b = self.L["ghost_planes_below"] * self.plane
+        return local[b:b + self.L["n_owned"]]
+
+    def _spikes(self, s):
+        Mq, p = self.Ms[self.dim - 1], self.p
+        pb, pe = self.slabs[s]
+        A = Mq[pb:pe, pb:pe]
+        V = np.linalg.solve(A, Mq[pb:pe, pe:pe + p]) if pe < Mq.shape[0] else np.zeros((pe - pb, p))
+        W = np.linalg.solve(A, Mq[pb:pe, pb - p:pb]) if pb > 0 else np.zeros((pe - pb, p))
+        return A, V, W
+
+    def mass_solve_slab(self, rhs, x):
+        A, _, _ = self._spikes(self.rank)
+        v = rhs.numpy().reshape(A.shape[0], self.plane)
+        v = np.linalg.solve(A, v)
+        if self.dim >= 2:
+            inner = self.Ms[0] if self.dim == 2 else np.kron(self.Ms[1], self.Ms[0])
+            v = np.linalg.solve(inner, v.T).T
+        x.numpy()[:] = v.reshape(-1)
+        return x
+
+    def mass_solve_interface(self, x_local):
+        p, P, r = self.p, self.plane, self.rank
+        gb = self.L["ghost_planes_below"]
+        a = x_local.numpy().reshape(-1, P)
+        n = self.slabs[r][1] - self.slabs[r][0]
+        own = a[gb:gb + n]
+        _, V, W = self._spikes(r)
+        b = np.zeros((p, P))
+        t = np.zeros((p, P))
+        if r > 0:
+            _, Vl, _ = self._spikes(r - 1)
+            S = np.block([[np.eye(p), Vl[-p:]], [W[:p], np.eye(p)]])
+            b = np.linalg.solve(S, np.concatenate([a[gb - p:gb], own[:p]]))[:p]
+        if r + 1 < self.world:
+            _, _, Wh = self._spikes(r + 1)
+            S = np.block([[np.eye(p), V[-p:]], [Wh[:p], np.eye(p)]])
+            t = np.linalg.solve(S, np.concatenate([own[-p:], a[gb + n:gb + n + p]]))[p:]
+        own -= V @ t + W @ b
+        return x_local
+
+
+def _spike_worker(rank, world, port, dim, p, n, q):
+    import torch
+    import torch.distributed as dist
+    from gdm_amd.distributed import HaloExchange, SlabMassSolve
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        op = _NpSpikeOp(dim, p, n, world, rank)
+        halo = HaloExchange(n[dim - 1], world, rank, op.plane, p)
+        m = O.Mesh(dim, p, list(n))
+        r = np.random.default_rng(11).uniform(-1, 1, m.n_dofs)
+        L = op.L
+        mine = torch.from_numpy(r[L["owned_plane_begin"] * op.plane:L["owned_plane_end"] * op.plane].copy())
+        x_local = torch.zeros(L["n_local"], dtype=torch.float64)
+        x = SlabMassSolve(op, halo).solve(mine, x_local)
+        q.put((rank, L["owned_plane_begin"] * op.plane, x.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,dim,p,n", [(2, 2, 3, (5, 200)), (3, 2, 5, (5, 240)), (4, 1, 3, (400,)),
+                                           (2, 3, 3, (3, 3, 150))])
+def test_slab_mass_solve_gloo(world, dim, p, n):
+    """Distributed exact mass inverse by slab-local solves + one p-plane
+    exchange + the 2p x 2p interface systems (SlabMassSolve over gloo, numpy
+    test double of the device steps) == the global Kronecker inverse; the
+    library's pure-host gdm_mass_spike_eps reports the dropped coupling the
+    numpy spikes show."""
+    import torch.multiprocessing as mp
+
+    eps = _capi.mass_spike_eps(dim, p, list(n), world)
+    assert eps < 1e-15
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spike_worker, args=(r, world, port, dim, p, n, q)) for r in range(world)]
+    for p_ in procs:
+        p_.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p_ in procs:
+        p_.join(120)
+    assert all(p_.exitcode == 0 for p_ in procs), [p_.exitcode for p_ in procs]
+    m = O.Mesh(dim, p, list(n))
+    r = np.random.default_rng(11).uniform(-1, 1, m.n_dofs)
+    ref = m.kron_mass_inverse(r)
+    x = np.zeros_like(ref)
+    for _, off, v in res:
+        x[off:off + len(v)] = v
+    assert np.linalg.norm(x - ref) / np.linalg.norm(ref) < 1e-12
+
+
+@pytest.mark.parametrize("dim,p,n,world", [(2, 3, (5, 60), 2), (1, 5, (120,), 3), (3, 7, (7, 7, 255), 4),
+                                           (3, 7, (7, 7, 255), 8)])
+def test_mass_spike_eps_matches_numpy(dim, p, n, world):
+    """gdm_mass_spike_eps (C++ host math) == the largest far-spike entry of
+    the numpy restatement; thin slabs (C4, 8 ranks: 32 planes at p = 7) are
+    reported above the 1e-15 the solve accepts."""
+    ops = [_NpSpikeOp(dim, p, n, world, s) for s in range(world)]
+    eps = 0.0
+    for s, op in enumerate(ops):
+        _, V, W = op._spikes(s)
+        if s > 0:
+            eps = max(eps, np.abs(W[-p:]).max())
+        if s + 1 < world:
+            eps = max(eps, np.abs(V[:p]).max())
+    got = _capi.mass_spike_eps(dim, p, list(n), world)
+    assert got == pytest.approx(eps, rel=1e-6, abs=1e-300)
+    if (dim, p, world) == (3, 7, 8):
+        assert got > 1e-15
