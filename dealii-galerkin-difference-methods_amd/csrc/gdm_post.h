@@ -25,7 +25,7 @@ struct ErrGeom {
 }  // namespace gdmk
 
 extern "C" {
-size_t gdmk_error_norms_lds_bytes(int p);
+size_t gdmk_error_norms_lds_bytes(int p, int dim);
 // S: [max(1, p)][p+1][p+1] shape values phi^cat_i(xq_q); out3 (device) =
 // (Linf, L1, L2^2) of the owned cells; partial: 3 * n_partial doubles
 hipError_t gdmk_launch_error_norms(const gdmk::ErrGeom &g, const gdmk::BcFn &f, double t, const double *S,

@@ -50,111 +50,135 @@ __device__ __forceinline__ double sine_1d(const BcFn &f, int e, double x, double
 
 }  // namespace
 
-// LDS: row[nb2][nb1][W] | w[nq2][nq1][W] | S[ncat][n1][n1] | fx[CX][n1] | fy[n1] | fz[n1] ; W = CX + p
+// LDS: A = row[NB2][NB1][W] (later w[NQ2][NQ1][W]) | B = tz[NQ2][NB1][W] |
+//      S[NCAT][N1][N1] | fx[CX][N1] | fy[N1] | fz[N1] | cacc[TPC][CX] ; W = CX + P
+template <int P, int DIM>
 __global__ void __launch_bounds__(NT) error_norms_kernel(ErrGeom g, BcFn f, double t, const double *__restrict__ S,
                                                          const double *__restrict__ u, double *__restrict__ cell_err,
                                                          double *__restrict__ partial) {
+  constexpr int N1 = P + 1, W = CX + P;
+  constexpr int NB1 = DIM > 1 ? N1 : 1, NB2 = DIM > 2 ? N1 : 1;  // = quadrature points per direction
+  constexpr int NCAT = P > 1 ? P : 1;
   extern __shared__ double lds[];
-  const int p = g.p, n1 = p + 1, W = CX + p;
-  const int nb1 = g.nb[1], nb2 = g.nb[2], nq0 = g.nq[0], nq1 = g.nq[1], nq2 = g.nq[2];
-  const int ncat = max(1, p);
-  double *row = lds;
-  double *w = row + (size_t)nb2 * nb1 * W;
-  double *Sl = w + (size_t)nq2 * nq1 * W;
-  double *fx = Sl + (size_t)ncat * n1 * n1;
-  double *fy = fx + CX * n1;
-  double *fz = fy + n1;
+  double *A = lds;
+  double *B = A + NB2 * NB1 * W;
+  double *Sl = B + NB2 * NB1 * W;
+  double *fx = Sl + NCAT * N1 * N1;
+  double *fy = fx + CX * N1;
+  double *fz = fy + N1;
+  double *cacc = fz + N1;
   const int tid = threadIdx.x;
-  for (int i = tid; i < ncat * n1 * n1; i += NT) Sl[i] = S[i];
+  for (int i = tid; i < NCAT * N1 * N1; i += NT) Sl[i] = S[i];
+  double wq[N1];
+#pragma unroll
+  for (int q = 0; q < N1; ++q) wq[q] = g.wq[q];
 
   const int ncx = g.ce[0] - g.cb[0], ncy = g.ce[1] - g.cb[1], ncz = g.ce[2] - g.cb[2];
   const int chunks = (ncx + CX - 1) / CX;
   const int64_t n_items = (int64_t)chunks * ncy * ncz;
-  const int npts = nq0 * nq1 * nq2;
   double a_l1 = 0.0, a_l2 = 0.0, a_inf = 0.0;
+  const int cl = tid % CX, grp = tid / CX;  // point phase: cell of the chunk, line group
 
   for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     const int chunk = (int)(item % chunks);
     const int64_t r = item / chunks;
     const int cy = g.cb[1] + (int)(r % ncy), cz = g.cb[2] + (int)(r / ncy);
     const int cx0 = g.cb[0] + chunk * CX, nc = min(CX, g.ce[0] - cx0);
-    const int xb = box_offset_d(cx0, p, g.ncell[0]);
-    const int wdt = box_offset_d(cx0 + nc - 1, p, g.ncell[0]) + p + 1 - xb;
-    const int oy = g.dim > 1 ? box_offset_d(cy, p, g.ncell[1]) : 0;
-    const int oz = g.dim > 2 ? box_offset_d(cz, p, g.ncell[2]) : 0;
-    const int caty = g.dim > 1 ? category_d(cy, p, g.ncell[1]) : 0;
-    const int catz = g.dim > 2 ? category_d(cz, p, g.ncell[2]) : 0;
-    __syncthreads();  // previous item's LDS reads are done
+    const int xb = box_offset_d(cx0, P, g.ncell[0]);
+    const int wdt = box_offset_d(cx0 + nc - 1, P, g.ncell[0]) + P + 1 - xb;
+    const int oy = DIM > 1 ? box_offset_d(cy, P, g.ncell[1]) : 0;
+    const int oz = DIM > 2 ? box_offset_d(cz, P, g.ncell[2]) : 0;
+    const double *Sy = Sl + (DIM > 1 ? category_d(cy, P, g.ncell[1]) : 0) * N1 * N1;
+    const double *Sz = Sl + (DIM > 2 ? category_d(cz, P, g.ncell[2]) : 0) * N1 * N1;
+    __syncthreads();  // the previous item's LDS reads are done
     // stage the DoF box rows (x contiguous: coalesced)
-    for (int i = tid; i < nb2 * nb1 * wdt; i += NT) {
-      const int x = i % wdt, yz = i / wdt, iy = yz % nb1, iz = yz / nb1;
+    for (int i = tid; i < NB2 * NB1 * wdt; i += NT) {
+      const int x = i % wdt, yz = i / wdt, iy = yz % NB1, iz = yz / NB1;
       const int64_t gi = (int64_t)(xb + x) + g.N0 * ((int64_t)(oy + iy) + g.N1 * (int64_t)(oz + iz));
-      row[(size_t)yz * W + x] = u[gi - g.base];
+      A[yz * W + x] = u[gi - g.base];
     }
     if (f.kind == 2) {
-      for (int i = tid; i < nc * nq0; i += NT) {
-        const int c = i / nq0, q = i % nq0;
-        fx[c * n1 + q] = sine_1d(f, 0, g.lo[0] + (cx0 + c + g.xq[q]) * g.h[0], t);
+      for (int i = tid; i < nc * N1; i += NT) {
+        const int c = i / N1, q = i % N1;
+        fx[c * N1 + q] = sine_1d(f, 0, g.lo[0] + (cx0 + c + g.xq[q]) * g.h[0], t);
       }
-      if (tid < nq1) fy[tid] = g.dim > 1 ? sine_1d(f, 1, g.lo[1] + (cy + g.xq[tid]) * g.h[1], t) : 1.0;
-      if (tid >= 64 && tid - 64 < nq2) fz[tid - 64] = g.dim > 2 ? sine_1d(f, 2, g.lo[2] + (cz + g.xq[tid - 64]) * g.h[2], t) : 1.0;
+      if (tid < N1) fy[tid] = DIM > 1 ? sine_1d(f, 1, g.lo[1] + (cy + g.xq[tid]) * g.h[1], t) : 1.0;
+      if (tid >= 64 && tid < 64 + N1) fz[tid - 64] = DIM > 2 ? sine_1d(f, 2, g.lo[2] + (cz + g.xq[tid - 64]) * g.h[2], t) : 1.0;
     }
     __syncthreads();
-    // contract z and y: w[qz][qy][x] = sum_iz sum_iy Sz[iz][qz] Sy[iy][qy] row[iz][iy][x]
-    for (int i = tid; i < nq2 * nq1 * wdt; i += NT) {
-      const int x = i % wdt, qq = i / wdt, qy = qq % nq1, qz = qq / nq1;
-      double acc = 0.0;
-      for (int iz = 0; iz < nb2; ++iz) {
-        const double sz = g.dim > 2 ? Sl[(catz * n1 + iz) * n1 + qz] : 1.0;
+    const double *w = A;
+    if (DIM == 3) {  // B[qz][iy][x] = sum_iz Sz[iz][qz] A[iz][iy][x]
+      for (int i = tid; i < NB2 * NB1 * W; i += NT) {
+        const int x = i % W, qi = i / W, iy = qi % NB1, qz = qi / NB1;
         double s = 0.0;
-        for (int iy = 0; iy < nb1; ++iy) {
-          const double sy = g.dim > 1 ? Sl[(caty * n1 + iy) * n1 + qy] : 1.0;
-          s = fma(sy, row[(size_t)(iz * nb1 + iy) * W + x], s);
-        }
-        acc = fma(sz, s, acc);
+#pragma unroll
+        for (int iz = 0; iz < NB2; ++iz) s = fma(Sz[iz * N1 + qz], A[(iz * NB1 + iy) * W + x], s);
+        B[i] = s;
       }
-      w[(size_t)qq * W + x] = acc;
+      __syncthreads();
     }
-    __syncthreads();
-    // points: TPC lanes per cell
-    const int cl = tid / TPC, sub = tid % TPC;
+    if (DIM >= 2) {  // A[qz][qy][x] = sum_iy Sy[iy][qy] src[qz][iy][x]
+      const double *src = DIM == 3 ? B : A;
+      double *dst = DIM == 3 ? A : B;
+      for (int i = tid; i < NB2 * NB1 * W; i += NT) {
+        const int x = i % W, qi = i / W, qy = qi % NB1, qz = qi / NB1;
+        double s = 0.0;
+#pragma unroll
+        for (int iy = 0; iy < NB1; ++iy) s = fma(Sy[iy * N1 + qy], src[(qz * NB1 + iy) * W + x], s);
+        dst[i] = s;
+      }
+      __syncthreads();
+      w = dst;
+    }
+    // points: one (qy, qz) line of N1 points per step, TPC line groups per cell
     double c_l2 = 0.0;
     if (cl < nc) {
       const int cx = cx0 + cl;
-      const int catx = category_d(cx, p, g.ncell[0]);
-      const int ox = box_offset_d(cx, p, g.ncell[0]) - xb;
-      for (int pt = sub; pt < npts; pt += TPC) {
-        const int qx = pt % nq0, qy = (pt / nq0) % nq1, qz = pt / (nq0 * nq1);
-        const double *wr = w + (size_t)(qz * nq1 + qy) * W + ox;
-        double v = 0.0;
-        for (int ix = 0; ix < n1; ++ix) v = fma(Sl[(catx * n1 + ix) * n1 + qx], wr[ix], v);
-        double ex;
-        if (f.kind == 0) {
-          ex = f.prm[0];
-        } else if (f.kind == 1) {
-          const double xc[3] = {g.lo[0] + (cx + g.xq[qx]) * g.h[0], g.lo[1] + (cy + g.xq[qy]) * g.h[1],
-                                g.lo[2] + (cz + g.xq[qz]) * g.h[2]};
-          double r2 = 0.0;
-          for (int d = 0; d < g.dim; ++d) r2 += (xc[d] - f.prm[1 + d]) * (xc[d] - f.prm[1 + d]);
-          ex = fmax(0.0, f.prm[0] - sqrt(r2));
-        } else {
-          ex = fx[cl * n1 + qx] * fy[qy] * fz[qz];
+      const double *Sx = Sl + category_d(cx, P, g.ncell[0]) * N1 * N1;
+      const int ox = box_offset_d(cx, P, g.ncell[0]) - xb;
+      for (int l = grp; l < NB1 * NB2; l += TPC) {
+        const int qy = l % NB1, qz = l / NB1;
+        const double *wr = w + l * W + ox;
+        double wv[N1];
+#pragma unroll
+        for (int ix = 0; ix < N1; ++ix) wv[ix] = wr[ix];
+        const double wyz = g.jxw * (DIM > 1 ? wq[qy] : 1.0) * (DIM > 2 ? wq[qz] : 1.0);
+        const double fyz = f.kind == 2 ? fy[qy] * fz[qz] : 0.0;
+#pragma unroll
+        for (int qx = 0; qx < N1; ++qx) {
+          double v = 0.0;
+#pragma unroll
+          for (int ix = 0; ix < N1; ++ix) v = fma(Sx[ix * N1 + qx], wv[ix], v);
+          double ex;
+          if (f.kind == 2) {
+            ex = fx[cl * N1 + qx] * fyz;
+          } else if (f.kind == 1) {
+            const double d0 = g.lo[0] + (cx + g.xq[qx]) * g.h[0] - f.prm[1];
+            const double d1 = DIM > 1 ? g.lo[1] + (cy + g.xq[qy]) * g.h[1] - f.prm[2] : 0.0;
+            const double d2 = DIM > 2 ? g.lo[2] + (cz + g.xq[qz]) * g.h[2] - f.prm[3] : 0.0;
+            ex = fmax(0.0, f.prm[0] - sqrt(d0 * d0 + d1 * d1 + d2 * d2));
+          } else {
+            ex = f.prm[0];
+          }
+          const double e = v - ex, ae = fabs(e), jxw = wyz * wq[qx];
+          c_l2 = fma(e * e, jxw, c_l2);
+          a_l1 = fma(ae, jxw, a_l1);
+          a_inf = fmax(a_inf, ae);
         }
-        const double e = v - ex, ae = fabs(e);
-        const double jxw = g.jxw * g.wq[qx] * (g.dim > 1 ? g.wq[qy] : 1.0) * (g.dim > 2 ? g.wq[qz] : 1.0);
-        c_l2 = fma(e * e, jxw, c_l2);
-        a_l1 = fma(ae, jxw, a_l1);
-        a_inf = fmax(a_inf, ae);
       }
     }
     a_l2 += c_l2;
-    // the cell's TPC lanes are consecutive in one wave
-    double s = c_l2;
-    for (int m = 1; m < TPC; m <<= 1) s += __shfl_xor(s, m);
-    if (cell_err && cl < nc && sub == 0) {
-      const int64_t ci = (int64_t)(cx0 + cl - g.cb[0]) +
-                         (int64_t)ncx * ((int64_t)(cy - g.cb[1]) + (int64_t)ncy * (int64_t)(cz - g.cb[2]));
-      cell_err[ci] = sqrt(s);
+    if (cell_err) {
+      cacc[grp * CX + cl] = c_l2;
+      __syncthreads();
+      if (tid < nc) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < TPC; ++k) s += cacc[k * CX + tid];
+        const int64_t ci = (int64_t)(cx0 + tid - g.cb[0]) +
+                           (int64_t)ncx * ((int64_t)(cy - g.cb[1]) + (int64_t)ncy * (int64_t)(cz - g.cb[2]));
+        cell_err[ci] = sqrt(s);
+      }
     }
   }
   // block reduction of (Linf, L1, L2^2)
@@ -215,22 +239,55 @@ __global__ void __launch_bounds__(256) error_reduce_kernel(int n, const double *
 
 }  // namespace gdmk
 
-extern "C" size_t gdmk_error_norms_lds_bytes(int p) {
+extern "C" size_t gdmk_error_norms_lds_bytes(int p, int dim) {
   const int n1 = p + 1, W = gdmk::CX + p, ncat = std::max(1, p);
-  return sizeof(double) * ((size_t)2 * n1 * n1 * W + (size_t)ncat * n1 * n1 + (size_t)gdmk::CX * n1 + 2 * n1);
+  const int nb1 = dim > 1 ? n1 : 1, nb2 = dim > 2 ? n1 : 1;
+  return sizeof(double) * ((size_t)2 * nb1 * nb2 * W + (size_t)ncat * n1 * n1 + (size_t)gdmk::CX * n1 + 2 * n1 +
+                           (size_t)gdmk::TPC * gdmk::CX);
 }
+
+namespace {
+template <int P, int DIM>
+hipError_t launch_err(const gdmk::ErrGeom &g, const gdmk::BcFn &f, double t, const double *S, const double *u,
+                      double *cell_err, double *partial, int n_partial, hipStream_t st) {
+  const size_t lds = gdmk_error_norms_lds_bytes(P, DIM);
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gdmk::error_norms_kernel<P, DIM>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((gdmk::error_norms_kernel<P, DIM>), dim3((unsigned)n_partial), dim3(gdmk::NT), lds, st, g, f, t,
+                     S, u, cell_err, partial);
+  return hipSuccess;
+}
+template <int P>
+hipError_t launch_err_dim(const gdmk::ErrGeom &g, const gdmk::BcFn &f, double t, const double *S, const double *u,
+                          double *cell_err, double *partial, int n_partial, hipStream_t st) {
+  switch (g.dim) {
+    case 1: return launch_err<P, 1>(g, f, t, S, u, cell_err, partial, n_partial, st);
+    case 2: return launch_err<P, 2>(g, f, t, S, u, cell_err, partial, n_partial, st);
+    default: return launch_err<P, 3>(g, f, t, S, u, cell_err, partial, n_partial, st);
+  }
+}
+}  // namespace
 
 extern "C" hipError_t gdmk_launch_error_norms(const gdmk::ErrGeom &g, const gdmk::BcFn &f, double t,
                                              const double *S, const double *u, double *cell_err, double *partial,
                                              int n_partial, double *out3, hipStream_t st) {
-  const size_t lds = gdmk_error_norms_lds_bytes(g.p);
-  if (lds > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gdmk::error_norms_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
+  hipError_t e;
+  switch (g.p) {
+    case 1: e = launch_err_dim<1>(g, f, t, S, u, cell_err, partial, n_partial, st); break;
+    case 2: e = launch_err_dim<2>(g, f, t, S, u, cell_err, partial, n_partial, st); break;
+    case 3: e = launch_err_dim<3>(g, f, t, S, u, cell_err, partial, n_partial, st); break;
+    case 4: e = launch_err_dim<4>(g, f, t, S, u, cell_err, partial, n_partial, st); break;
+    case 5: e = launch_err_dim<5>(g, f, t, S, u, cell_err, partial, n_partial, st); break;
+    case 6: e = launch_err_dim<6>(g, f, t, S, u, cell_err, partial, n_partial, st); break;
+    case 7: e = launch_err_dim<7>(g, f, t, S, u, cell_err, partial, n_partial, st); break;
+    case 8: e = launch_err_dim<8>(g, f, t, S, u, cell_err, partial, n_partial, st); break;
+    case 9: e = launch_err_dim<9>(g, f, t, S, u, cell_err, partial, n_partial, st); break;
+    default: return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(gdmk::error_norms_kernel, dim3((unsigned)n_partial), dim3(gdmk::NT), lds, st, g, f, t, S, u,
-                     cell_err, partial);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(gdmk::error_reduce_kernel, dim3(1), dim3(256), 0, st, n_partial, partial, out3);
   return hipGetLastError();
 }
