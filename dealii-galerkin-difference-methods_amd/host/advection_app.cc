@@ -14,7 +14,8 @@
 // instead of the host callbacks.  NRANKS > 1 runs the multi-rank path: one
 // thread per rank (z-slabs of system.h:720-757, all on DEVICE), ghost planes
 // and dots through GDM::HIP::ThreadGroup (an MPI communicator's role), the
-// distributed CG mass solve; OUT holds the ranks' owned values in rank order.
+// distributed exact mass inverse (SPIKE) when the slabs are thick enough, else
+// the distributed Jacobi CG; OUT holds the ranks' owned values in rank order.
 // With DEVBC the final errors against the exact solution are computed on the
 // device (AdvectionProblem::postprocess -> gdm_error_norms) and printed in the
 // reference's postprocess format (time, L2, L1, Linf).
@@ -85,6 +86,7 @@ int run(int p, int n, int steps, double cfl, const char *out, int device, int de
   std::vector<double> u;
   unsigned int done = 0;
   std::array<double, 6> norms{{-1.0, -1.0, -1.0, 0.0, 0.0, 0.0}};
+  bool spike = false;
   if (n_ranks <= 1) {
     GDM::HIP::AdvectionProblem<dim> problem(make_params<dim>(p, n, cfl, device, devbc));
     done = problem.run(steps);
@@ -125,6 +127,7 @@ int run(int p, int n, int steps, double cfl, const char *out, int device, int de
             const std::array<double, 6> e = problem.postprocess(time_of(steps_done[r], n, cfl));
             if (r == 0) norms = e;
           }
+          if (r == 0) spike = problem.used_spike_solve();
         } catch (const std::exception &e) {
           errors[r] = e.what();
           std::fprintf(stderr, "rank %d: %s\n", r, e.what());
@@ -138,6 +141,7 @@ int run(int p, int n, int steps, double cfl, const char *out, int device, int de
   double s = 0.0;
   for (double v : u) s += v * v;
   std::printf("steps %u  |u|_2 %.15e\n", done, std::sqrt(s));
+  if (n_ranks > 1) std::printf("mass solve: %s\n", spike ? "spike" : "cg");
   if (devbc)  // the reference's postprocess line (problem.h:427-433): counter, time, L2, L1, Linf
     std::printf("%5d %8.5f %14.8e %14.8e %14.8e\n", 0, time_of(done, n, cfl), norms[2], norms[1], norms[0]);
   std::ofstream f(out, std::ios::binary);

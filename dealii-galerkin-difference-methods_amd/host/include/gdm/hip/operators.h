@@ -390,6 +390,23 @@ class MassMatrixOperator {
     }
     return it;
   }
+  // Multi-rank exact solve (the truncated SPIKE scheme of
+  // gdm_mass_solve_slab / gdm_mass_solve_interface): slab-local solve, one
+  // ghost-plane exchange through `comm`, interface correction.  Usable when
+  // spike_available() (slabs thick enough for the dropped coupling to stay
+  // below 1e-15); x_owned may alias b_owned.
+  bool spike_available() const {
+    double eps = 1.0;
+    return gdm_mass_spike_eps(&discretization.get_mesh(), &eps) == GDM_OK && eps <= 1e-15;
+  }
+  void solve_spike(double *x_owned, const double *b_owned, Communicator &comm) const {
+    if (sp_x.size() != (std::size_t)layout.n_local) sp_x.reinit(op, layout.n_local);
+    double *own = sp_x.get_values() + layout.ghost_planes_below * layout.plane_size;
+    check(gdm_mass_solve_slab(op, b_owned, own), "gdm_mass_solve_slab");
+    comm.update_ghost_values(op, sp_x);
+    check(gdm_mass_solve_interface(op, sp_x.get_values()), "gdm_mass_solve_interface");
+    check(gdm_memcpy_d2d(op, x_owned, own, sizeof(double) * layout.n_owned), "gdm_memcpy_d2d");
+  }
   gdm_op *handle() const { return op; }
 
  private:
@@ -397,6 +414,7 @@ class MassMatrixOperator {
   gdm_op *op = nullptr;
   gdm_layout layout{};
   mutable DeviceVector cg_p, cg_r, cg_z, cg_Ap, cg_invdiag;  // solve_distributed work vectors
+  mutable DeviceVector sp_x;                                  // solve_spike local vector
 };
 
 // deal.II DiscreteTime: fixed steps, the last one shrunk to hit end_t or, when
@@ -450,12 +468,15 @@ class AdvectionProblem {
     stiffness_matrix_operator.initialize_dof_vector(acc);
     stiffness_matrix_operator.initialize_dof_vector(stage);
     if (params.n_ranks != 1) rhs_tmp.reinit(stiffness_matrix_operator.handle(), stiffness_matrix_operator.get_layout().n_owned);
+    use_spike = params.n_ranks != 1 && mass_matrix_operator.spike_available();
     const auto fu_rhs = [&](double time, BlockVector &y, BlockVector &result) {
       if (params.n_ranks != 1) comm->update_ghost_values(stiffness_matrix_operator.handle(), y.block(1));
       stiffness_matrix_operator.compute_rhs(result, y, time);
       double *r = stiffness_matrix_operator.owned(result.block(1));
       if (params.n_ranks == 1) {
         mass_matrix_operator.solve(r, r);
+      } else if (use_spike) {
+        mass_matrix_operator.solve_spike(r, r, *comm);
       } else {
         check(gdm_memcpy_d2d(stiffness_matrix_operator.handle(), rhs_tmp.get_values(), r,
                              sizeof(double) * rhs_tmp.size()),
@@ -487,6 +508,8 @@ class AdvectionProblem {
     return std::vector<double>(v.begin() + o, v.begin() + o + L.n_owned);
   }
   const BlockVector &get_solution_vector() const { return solution; }
+  // which multi-rank mass solve run() used: exact SPIKE or the Jacobi CG
+  bool used_spike_solve() const { return use_spike; }
 
   // postprocess(time, solution) (problem.h:269-485), error part on the device:
   // {Linf, L1, L2, Linf_face, L1_face, L2_face} of u - exact_solution(time)
@@ -541,6 +564,7 @@ class AdvectionProblem {
   StiffnessMatrixOperator<dim> stiffness_matrix_operator;
   BlockVector solution;
   DeviceVector rhs_tmp;
+  bool use_spike = false;
 };
 
 }  // namespace HIP

@@ -157,7 +157,7 @@ def test_wave_driver_rk4_matches_oracle(tmp_path, dim, p, n, steps, nitsche):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dim,p,n,steps", [(2, 5, 30, 2), (3, 5, 14, 2), (3, 3, 20, 2)])
+@pytest.mark.parametrize("dim,p,n,steps", [(2, 5, 30, 2), (3, 5, 14, 2), (3, 3, 20, 2), (2, 5, 240, 2)])
 @pytest.mark.parametrize("n_ranks", [2, 3])
 def test_driver_multirank_matches_single_rank(tmp_path, dim, p, n, steps, n_ranks):
     """The C++ mirror's AdvectionProblem at n_ranks = 2, 3 (z-slabs of
@@ -174,6 +174,8 @@ def test_driver_multirank_matches_single_rank(tmp_path, dim, p, n, steps, n_rank
     u1, un = np.fromfile(out1, dtype=np.float64), np.fromfile(outn, dtype=np.float64)
     assert u1.shape == un.shape
     assert np.linalg.norm(un - u1) / np.linalg.norm(u1) < 1e-10
+    # thick slabs use the exact SPIKE inverse, thin ones the Jacobi CG
+    assert ("mass solve: spike" in r.stdout) == (_capi.mass_spike_eps(dim, p, n, n_ranks) <= 1e-15), r.stdout
     # postprocess reduced over the ranks (max / sum / sqrt-sum-sq) = one rank
     e1 = [float(v) for v in r1.stdout.strip().splitlines()[-1].split()[2:]]
     en = [float(v) for v in r.stdout.strip().splitlines()[-1].split()[2:]]
