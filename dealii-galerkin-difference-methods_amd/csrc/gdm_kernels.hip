@@ -643,31 +643,53 @@ struct XWall {
   int o[NI];  // AB offset, -1: none
 };
 
+// per-lane item geometry of the x-wall corrections, independent of the plane
+// and (up to 4 g rows) of the row group: computed once per tile, so the plane
+// loop carries no integer division
+template <int P, int BK>
+struct XWallPre {
+  static constexpr int NI = XWall<P, BK>::NI;
+  int u[NI], o[NI], c[NI], rr[NI];  // u-row offset, AB offset, table offset at g = 0; rr < 0: no item
+};
+
 template <int P, int R, int NC, int NP, int BK>
-__device__ __forceinline__ void xwall8_calc(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g,
-                                            XWall<P, BK> &xw) {
+__device__ __forceinline__ void xwall8_pre(const StencilArgs &a, const Tile7 &t, XWallPre<P, BK> &pre) {
   using G = Geom8<P, R, NC, NP, BK>;
-  constexpr int W = G::W, RL = G::RL, TX = G::TX, NCOMP = XWall<P, BK>::NCOMP;
+  constexpr int W = G::W, RL = G::RL, NCOMP = XWall<P, BK>::NCOMP;
   const int nitems = 4 * t.ncw * NCOMP;
 #pragma unroll
   for (int it = 0; it < XWall<P, BK>::NI; ++it) {
     const int e = t.lane + 64 * it;
-    xw.o[it] = -1;
-    xw.v[it] = 0.0;
     const int comp = e % NCOMP, rest = e / NCOMP;
     const int idx = rest % max(t.ncw, 1), rr = rest / max(t.ncw, 1);
-    const int r = 4 * g + rr;
-    if (e < nitems && r < G::UR) {
-      const int x = idx < t.nl ? t.x0 + idx : t.rs + (idx - t.nl);
-      const int cs = x < a.x_corr_left ? x : (P + 1) + (x - (a.Nx - a.x_corr_right));
-      const int lx = x - t.x0;
-      lcdouble *ur = us + r * RL + lx + 1;  // tap k of column x
-      lcdouble *cm = t.corr + cs * 2 * W + comp * W;
+    const int x = idx < t.nl ? t.x0 + idx : t.rs + (idx - t.nl);
+    const int cs = x < a.x_corr_left ? x : (P + 1) + (x - (a.Nx - a.x_corr_right));
+    const int lx = x - t.x0;
+    pre.rr[it] = e < nitems ? rr : -1;
+    pre.u[it] = rr * RL + lx + 1;
+    pre.o[it] = G::ab(rr, lx) + (BK != 0 ? comp : 0);
+    pre.c[it] = cs * 2 * W + comp * W;
+  }
+}
+
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void xwall8_calc(const Tile7 &t, lcdouble *us, int g, const XWallPre<P, BK> &pre,
+                                            XWall<P, BK> &xw) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  constexpr int W = G::W, RL = G::RL;
+#pragma unroll
+  for (int it = 0; it < XWall<P, BK>::NI; ++it) {
+    xw.o[it] = -1;
+    xw.v[it] = 0.0;
+    if (pre.rr[it] >= 0 && 4 * g + pre.rr[it] < G::UR) {
+      lcdouble *ur = us + 4 * g * RL + pre.u[it];  // tap k of the wall column
+      lcdouble *cm = t.corr + pre.c[it];
       double d = 0.0;
 #pragma unroll
       for (int k = 0; k < W; ++k) d = fma(cm[k], ur[k], d);
       xw.v[it] = d;
-      xw.o[it] = G::ab(r, lx) + (BK != 0 ? comp : 0);
+      // rows 4g.. of AB: G::ab is linear in the row
+      xw.o[it] = 4 * g * G::ABRS + pre.o[it];
     }
   }
 }
@@ -759,6 +781,8 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
     if (k < n) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + k, u[k]);
   GDM_LDS_BARRIER();  // tables in LDS
   dpair V1[4];
+  XWallPre<P, BK> xpre;
+  if (t.ncw > 0) xwall8_pre<P, R, NC, NP, BK>(a, t, xpre);
   int slot = 0;
   for (int i = 0; i < n; ++i) {
     const int rem = n - 1 - i;  // planes issued after plane i (at most NS - 1)
@@ -778,8 +802,8 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
     if (two && !GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], t.wv + NP, V2);
     XWall<P, BK> xw0, xw1;
     if (t.ncw > 0) {
-      xwall8_calc<P, R, NC, NP, BK>(a, t, u[slot], t.wv, xw0);
-      if (two) xwall8_calc<P, R, NC, NP, BK>(a, t, u[slot], t.wv + NP, xw1);
+      xwall8_calc<P, R, NC, NP, BK>(t, u[slot], t.wv, xpre, xw0);
+      if (two) xwall8_calc<P, R, NC, NP, BK>(t, u[slot], t.wv + NP, xpre, xw1);
     }
     if (t.yedge && i > 0) {
       ywall8<P, R, NC, NP, BK>(a, t);  // corrections of plane i - 1 (AB still holds it)
@@ -799,7 +823,7 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
         if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], g, V1);
         write_ab8<P, R, NC, NP, BK>(t, g, V1);
         if (t.ncw > 0) {
-          xwall8_calc<P, R, NC, NP, BK>(a, t, u[slot], g, xw0);
+          xwall8_calc<P, R, NC, NP, BK>(t, u[slot], g, xpre, xw0);
           xwall8_add<P, BK>(t, xw0);
         }
       }
