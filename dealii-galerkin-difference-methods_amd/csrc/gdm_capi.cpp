@@ -17,7 +17,6 @@
 
 #include "../../include/gdm_hip.h"
 #include "gdm_coeffs.h"
-#include "gdm_faces.h"
 #include "gdm_kernels.h"
 #include "gdm_post.h"
 #include "gdm_rk.h"
@@ -781,30 +780,8 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
 void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
                           hipStream_t st = nullptr) {
   if (op->kind != GDM_OP_ADVECTION) return;
-  // phase 2 (after the fork/join): every face's step 2 in one launch when
-  // each face has its own scratch
-  gdmk::Step2Set s2{};
-  bool fused2 = phase == 2 && op->faces.size() <= 6;
-  for (const Face &F : op->faces)
-    if (F.scale != 0.0 && !F.T) fused2 = false;
   for (const Face &F : op->faces) {
     if (F.scale == 0.0) continue;
-    if (fused2) {
-      gdmk::Step2Face &g = s2.f[s2.n++];
-      g.T = F.T;
-      g.n0 = F.t0.node_end - F.t0.node_begin;
-      g.i1_begin = F.t1.node_begin;
-      g.i1_end = F.t1.node_end;
-      g.wmax1 = F.t1.wmax;
-      g.qs1 = F.t1.qs;
-      g.qc1 = F.t1.qc;
-      g.w1 = F.t1.w;
-      g.base = F.base;
-      g.stride0 = F.t0.stride;
-      g.stride1 = F.t1.stride;
-      g.scale = F.scale;
-      continue;
-    }
     gdmk::FaceArgs fa{};
     fa.U = bc_values + F.offset;
     fa.Q0 = F.t0.Q;
@@ -836,7 +813,6 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     fa.phase = phase;
     hip_check(gdmk_launch_face(fa, phase == 1 && st ? st : op->stream), "face launch");
   }
-  if (fused2 && s2.n > 0) hip_check(gdmk_launch_face_step2_multi(s2, dst_owned, op->stream), "face step 2");
 }
 
 int choose_zchunk(const gdm_op *op) {
