@@ -237,3 +237,35 @@ def test_config5_full_size_vs_convolution():
     A.vmult(Ay, y)
     A.vmult(Axy, x + 2 * y)
     assert float(torch.linalg.norm(Axy - Ax - 2 * Ay) / torch.linalg.norm(Axy)) < 1e-13
+
+
+@pytest.mark.parametrize("ghost_penalty", [True, False])
+def test_cut_poisson_01_device_cg_golden(ghost_penalty):
+    """Config-5 path on the reference's own cut-cell system: the cut-Poisson
+    matrix and rhs of prototypes/cut_poisson_01_gdm.cc (2D p=3, 64 cells,
+    unit-circle level set, Nitsche, ghost penalty; assembled by the 2D cut-cell
+    restatement oracle/cut2d.py, pinned to the same golden on the CPU) solved
+    by the device SpMV + SolverCG (identity, ReductionControl(n, 1e-10,
+    1e-6), :326-335): the L2 error of the device solution reproduces
+    prototypes/cut_poisson_01_gdm.output (ghost penalty: all printed digits;
+    without: to 1e-4 relative, the spread of the unstabilised CG iterate
+    under fp64 summation order, see tests/test_cut2d_golden.py)."""
+    import cut2d
+
+    sp = _sp()
+    P = cut2d.CutPoisson2D(3, 64, ghost_penalty=ghost_penalty)
+    rp, cols, vals, rhs = P.assemble()
+    _, its_ref = P.solve(rp, cols, vals, rhs)
+    n = len(rhs)
+    A = sp.SparseMatrix(rp, cols.astype(np.uint32), vals)
+    x = torch.zeros(n, dtype=torch.float64, device="cuda")
+    its, res = sp.solve_cg(A, x, dev(rhs), preconditioner="identity", max_it=n, abs_tol=1e-10, rel_tol=1e-6)
+    e = P.l2_error(host(x))
+    golden = 4.3420e-04 if ghost_penalty else 4.2303e-04
+    if ghost_penalty:
+        assert "%.4e" % e == "%.4e" % golden, e
+        assert abs(its - its_ref) <= 5, (its, its_ref)
+    else:
+        assert abs(e - golden) / golden < 1e-4, e
+        assert abs(its - its_ref) <= 20, (its, its_ref)
+    assert res <= 1e-6 * np.linalg.norm(rhs)
