@@ -1025,13 +1025,15 @@ void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
   const double *in = rhs_owned;
   const int wg = op->mass_max_wgs;
   const bool v3 = op->mass_version >= 3 && gdmk_mass3_chunk(op->p) > 0;
+  // timing experiment only (wrong results near the line ends): interior rows everywhere
+  static const bool notab = std::getenv("GDM_MASS_NOTAB") != nullptr;
   auto pass = [&](int ax, int dir_kind, int64_t len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,
                   const char *what) {
     const LineTables &t = tab[ax];
     const bool aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(x_owned)) & 15) == 0;
     if (v3 && t.l3 && (dir_kind == 1 || (len % 2 == 0 && aligned)))
       hip_check(gdmk_launch_mass3(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, t.l3, t.u3, t.d3,
-                                  t.cst.data(), t.row_lo, t.row_hi, op->stream),
+                                  t.cst.data(), notab ? 0 : t.row_lo, notab ? (1 << 29) : t.row_hi, op->stream),
                 what);
     else
       hip_check(gdmk_launch_mass_lines(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, t.lrow, t.invd,

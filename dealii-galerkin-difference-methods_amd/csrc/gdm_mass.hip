@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "gdm_kernels.h"
 
@@ -37,6 +38,7 @@ typedef __attribute__((address_space(4))) const double cdouble;
 __device__ __forceinline__ cdouble *cptr(const double *p) { return (cdouble *)(p); }
 typedef double dpair __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) dpair ldouble2;
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 namespace {
 
@@ -287,13 +289,30 @@ struct Geo3 {
   // strided: loads in flight per lane.  One chunk ahead: with the 2C-double
   // ring this runs one wave per SIMD, so the FIFO alone must cover the HBM
   // latency (Q * 512 B per wave; a 16-deep FIFO measured as latency-bound)
-  static constexpr int Q = P <= 5 ? C : C / 2;  // p = 7: 28 (one full chunk spills)
+#ifdef GDM_MASS_Q5
+  static constexpr int Q = P == 5 ? GDM_MASS_Q5 : (P < 5 ? C : C / 2);
+#else
+  // with the stores streamed between the loads (Ring3::fwd ST), load j waits
+  // for vmcnt <= ~2 Q: Q = C / 2 <= 31 keeps that within the 6-bit counter
+  static constexpr int Q = P <= 5 ? C / 2 : C / 4;  // p = 7: C / 2 spills to scratch
+#endif
   static constexpr int QL = 4;                // rows: LDS pair reads ahead
   static constexpr int UPR = (C + 2) / 2;     // rows: 16-B units per LDS row (pitch C + 2 doubles)
   static constexpr int TILE = 64 * UPR;       // rows: units per tile (= 64 x DMA instructions)
   static constexpr size_t lds_bytes() { return 2 * (size_t)TILE * 16; }
   static_assert(C % Q == 0 && C % 4 == 0, "chunk geometry");
 };
+
+#ifdef GDM_MASS_WPE
+#define GDM_MASS_STRIDED_ATTR __attribute__((amdgpu_waves_per_eu(GDM_MASS_WPE)))
+#else
+#define GDM_MASS_STRIDED_ATTR
+#endif
+
+// line-end chunks: 2 = per-group table / interior-row decision, 1 = tables for the whole chunk
+#ifndef GDM_MASS_EDGE_MODE
+#define GDM_MASS_EDGE_MODE 1
+#endif
 
 // compiler-only fence: the scheduler may not move instructions across it
 #define GDM_FENCE()                    \
@@ -328,27 +347,54 @@ struct Ring3 {
     if constexpr (TAB) asm volatile("" : "+s"(i));
     return i;
   }
+  // MODE 0: every row of the call is an interior (constant) row; 1: every row
+  // from the tables; 2: decided per group of 4 positions (wave-uniform
+  // branch), so only the groups that touch the ~p/2 + 30 special rows at the
+  // line ends pay the table loads (a chunk-level decision ran 5 of 11 chunk
+  // steps of a 512-line from the tables)
+  __device__ __forceinline__ bool fwd_const(int i_lo, int i_hi) const { return i_lo >= k.row_lo && i_hi <= k.row_hi; }
+  __device__ __forceinline__ bool bwd_const(int i_lo, int i_hi) const {
+    return i_lo >= k.row_lo && i_hi <= k.row_hi - P;
+  }
 
   // cur <- w of the chunk at base (b values from get(j), j chunk-local and
   // compile-time, increasing); prev = w of the previous chunk (zeros before
   // the line start)
-  template <bool TAB, class Get>
-  __device__ __forceinline__ void fwd(double (&cur)[C], const double (&prev)[C], int base, Get &&get) const {
+  // ST: cur holds the final values of an earlier chunk that are stored (put,
+  // ascending) just before the forward values overwrite them, so the stores
+  // stream one per position between the loads instead of in a burst of C
+  // (a burst of C stores on top of the load FIFO overflows the 6-bit vmcnt)
+  template <int MODE, bool ST = false, class Get, class Put>
+  __device__ __forceinline__ void fwd(double (&cur)[C], const double (&prev)[C], int base, Get &&get, Put &&put) const {
     int ib = base;
+    bool tabg = MODE == 1;
+    auto pos = [&](auto tab, int j) {
+      constexpr bool T = decltype(tab)::value;
+      const int i = ib + j;
+      if constexpr (ST) put(cur[j]);
+      double s = get(j) * dco<T>(i);
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        const int jj = j - P + q;
+        s = fma(-lco<T>(i, q), jj >= 0 ? cur[jj] : prev[C + jj], s);
+      }
+      cur[j] = s;
+    };
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       if (j % 4 == 0) {
         GDM_FENCE();
-        ib = grp<TAB>(base + j) - j;
+        ib = grp<MODE != 0>(base + j) - j;
+        if constexpr (MODE == 2) tabg = !fwd_const(base + j, base + j + 4);
       }
-      const int i = ib + j;
-      double s = get(j) * dco<TAB>(i);
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        const int jj = j - P + q;
-        s = fma(-lco<TAB>(i, q), jj >= 0 ? cur[jj] : prev[C + jj], s);
+      if constexpr (MODE == 2) {
+        if (tabg)
+          pos(std::true_type{}, j);
+        else
+          pos(std::false_type{}, j);
+      } else {
+        pos(std::integral_constant<bool, MODE == 1>{}, j);
       }
-      cur[j] = s;
     }
     GDM_FENCE();
   }
@@ -356,51 +402,89 @@ struct Ring3 {
   // the recurrence from zero at base + 2C - 1 and run it over `next` (the
   // following chunk's w, not modified); otherwise the state after the chunk is
   // zero (line end).
-  template <bool WARM, bool TAB>
+  template <bool WARM, int MODE, int WMODE = MODE>
   __device__ __forceinline__ void bwd(double (&out)[C], const double (&next)[C], int base) const {
     double t[P];  // x at positions base + C + q, slot q % P
 #pragma unroll
     for (int q = 0; q < P; ++q) t[q] = 0.0;
+    bool tabg = MODE == 1;
     if constexpr (WARM) {
       int ib = base + C;
-#pragma unroll
-      for (int q = C - 1; q >= 0; --q) {
-        if ((C - 1 - q) % 4 == 0) ib = grp<TAB>(base + C + q) - q;
+      auto wpos = [&](auto tab, int q) {
+        constexpr bool T = decltype(tab)::value;
         const int i = ib + q;
-        double s = next[q] * dco<TAB>(i);
+        double s = next[q] * dco<T>(i);
 #pragma unroll
         for (int m = P; m >= 1; --m)
-          if (q + m < C) s = fma(-uco<TAB>(i, m - 1), t[(q + m) % P], s);
+          if (q + m < C) s = fma(-uco<T>(i, m - 1), t[(q + m) % P], s);
         t[q % P] = s;
+      };
+#pragma unroll
+      for (int q = C - 1; q >= 0; --q) {
+        if ((C - 1 - q) % 4 == 0) {
+          ib = grp<WMODE != 0>(base + C + q) - q;
+          if constexpr (WMODE == 2) tabg = !bwd_const(base + C + q - 3, base + C + q + 1);
+        }
+        if constexpr (WMODE == 2) {
+          if (tabg)
+            wpos(std::true_type{}, q);
+          else
+            wpos(std::false_type{}, q);
+        } else {
+          wpos(std::integral_constant<bool, WMODE == 1>{}, q);
+        }
       }
     }
     int ib = base;
-#pragma unroll
-    for (int j = C - 1; j >= 0; --j) {
-      if ((C - 1 - j) % 4 == 0) ib = grp<TAB>(base + j) - j;
+    auto bpos = [&](auto tab, int j) {
+      constexpr bool T = decltype(tab)::value;
       const int i = ib + j;
-      double s = out[j] * dco<TAB>(i);
+      double s = out[j] * dco<T>(i);
 #pragma unroll
       for (int m = P; m >= 1; --m) {
         const int jj = j + m;
-        s = fma(-uco<TAB>(i, m - 1), jj < C ? out[jj] : t[(jj - C) % P], s);
+        s = fma(-uco<T>(i, m - 1), jj < C ? out[jj] : t[(jj - C) % P], s);
       }
       out[j] = s;
+    };
+#pragma unroll
+    for (int j = C - 1; j >= 0; --j) {
+      if ((C - 1 - j) % 4 == 0) {
+        ib = grp<MODE != 0>(base + j) - j;
+        if constexpr (MODE == 2) tabg = !bwd_const(base + j - 3, base + j + 1);
+      }
+      if constexpr (MODE == 2) {
+        if (tabg)
+          bpos(std::true_type{}, j);
+        else
+          bpos(std::false_type{}, j);
+      } else {
+        bpos(std::integral_constant<bool, MODE == 1>{}, j);
+      }
     }
     GDM_FENCE();
   }
   // one march step: forward chunk c into cur, then back-solve chunk c - 1
   // (prev) with the warm-up over cur
-  template <class Get>
-  __device__ __forceinline__ void step(double (&cur)[C], double (&prev)[C], int c, Get &&get) const {
+  template <bool ST = false, class Get, class Put>
+  __device__ __forceinline__ void step(double (&cur)[C], double (&prev)[C], int c, Get &&get, Put &&put) const {
     const int base = c * C;
-    if (base - C >= k.row_lo && base + C + P <= k.row_hi - P) {
-      fwd<false>(cur, prev, base, get);
-      bwd<true, false>(prev, cur, base - C);
-    } else {
-      fwd<true>(cur, prev, base, get);
-      bwd<true, true>(prev, cur, base - C);
-    }
+    // forward rows [base, base + C); warm-up rows [base, base + C) with their
+    // u rows; back-solved rows [base - C, base): each part takes the interior
+    // row from kernel arguments when all its rows hold it
+    if (fwd_const(base, base + C))
+      fwd<0, ST>(cur, prev, base, get, put);
+    else
+      fwd<GDM_MASS_EDGE_MODE, ST>(cur, prev, base, get, put);
+    const bool wc = bwd_const(base, base + C), mc = bwd_const(base - C, base);
+    if (wc && mc)
+      bwd<true, 0, 0>(prev, cur, base - C);
+    else if (mc)
+      bwd<true, 0, GDM_MASS_EDGE_MODE>(prev, cur, base - C);
+    else if (wc)
+      bwd<true, GDM_MASS_EDGE_MODE, 0>(prev, cur, base - C);
+    else
+      bwd<true, GDM_MASS_EDGE_MODE, GDM_MASS_EDGE_MODE>(prev, cur, base - C);
   }
 };
 
@@ -412,7 +496,7 @@ struct Ring3 {
 // the offsets are 64-bit SGPR values, the lane offset is 32-bit).  src may
 // equal dst.
 template <int P>
-__global__ void __launch_bounds__(64) mass3_strided_kernel(const double *src, double *dst, int len, int64_t stride,
+__global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel(const double *src, double *dst, int len, int64_t stride,
                                                            int64_t n_lines, int64_t A, int64_t B,
                                                            const double *__restrict__ lrow,
                                                            const double *__restrict__ urow,
@@ -422,24 +506,33 @@ __global__ void __launch_bounds__(64) mass3_strided_kernel(const double *src, do
   const R r{cptr(lrow), cptr(urow), cptr(invd), k};
   // lanes past n_lines repeat the last line (same values, same addresses)
   const int64_t line = min((int64_t)blockIdx.x * 64 + threadIdx.x, n_lines - 1);
-  // wave-uniform base (lane 0's line) + a 32-bit lane byte offset: one SGPR
-  // address + one shared offset VGPR per access (global_load saddr form)
+  // wave-uniform base (lane 0's line) + a 32-bit lane byte offset; the
+  // position offset is a running 32-bit SGPR (buffer soffset): one SALU per
+  // access instead of a 64-bit multiply-add chain per position
   const int64_t b0 = (line / A) * B + (line % A);
   const int64_t bw = ((int64_t)__builtin_amdgcn_readfirstlane((int)(b0 >> 32)) << 32) |
                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b0);
   const uint32_t lbyte = (uint32_t)(b0 - bw) * 8u;
-  // the uniform byte offset of a position passes through an opaque SGPR move,
-  // or LICM hoists every per-position address out of the march loop
-  auto at = [&](const double *v, int i) -> const double & {
-    int64_t o = (int64_t)i * stride * 8;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + bw), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + bw), 0, 0x7fffffff, 0x00020000);
+  const uint32_t s8 = (uint32_t)(stride * 8), last = (uint32_t)(len - 1) * s8;
+  uint32_t lo = 0, so = 0;  // byte offsets of the next load / store position
+  auto load = [&]() -> double {
+    uint32_t o = min(lo, last);
     asm volatile("" : "+s"(o));
-    return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(v + bw) + o + lbyte);
+    lo += s8;
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lbyte, o, 0));
+  };
+  auto put = [&](double v) {
+    uint32_t o = so;
+    asm volatile("" : "+s"(o));
+    so += s8;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rd, lbyte, o, 0);
   };
   double fifo[Q];
-  int cb = 0;  // base of the chunk being forward-solved
   auto get = [&](int j) -> double {
     const double b = fifo[j % Q];
-    fifo[j % Q] = at(src, min(cb + j + Q, len - 1));
+    fifo[j % Q] = load();
     return b;
   };
   auto store = [&](const double (&h)[C], int base) {
@@ -447,12 +540,12 @@ __global__ void __launch_bounds__(64) mass3_strided_kernel(const double *src, do
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         if (j % 8 == 0) GDM_FENCE();
-        const_cast<double &>(at(dst, base + j)) = h[j];
+        put(h[j]);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < C; ++j)
-        if (base + j < len) const_cast<double &>(at(dst, base + j)) = h[j];
+        if (base + j < len) put(h[j]);
     }
     GDM_FENCE();
   };
@@ -460,25 +553,29 @@ __global__ void __launch_bounds__(64) mass3_strided_kernel(const double *src, do
 #pragma unroll
   for (int j = 0; j < C; ++j) h1[j] = 0.0;
 #pragma unroll
-  for (int q = 0; q < Q; ++q) fifo[q] = at(src, min(q, len - 1));
-  r.template fwd<true>(h0, h1, 0, get);
+  for (int q = 0; q < Q; ++q) fifo[q] = load();
+  auto none = [](double) {};
+  // the final values of chunk c - 2 are stored by the forward sweep of chunk
+  // c (fwd<.., true>), the last one or two chunks explicitly
+  r.template fwd<GDM_MASS_EDGE_MODE>(h0, h1, 0, get, none);
   for (int c = 1;; c += 2) {
     if (c * C >= len) {
-      r.template bwd<false, true>(h0, h1, (c - 1) * C);
+      if (c > 1) store(h1, (c - 2) * C);
+      r.template bwd<false, GDM_MASS_EDGE_MODE>(h0, h1, (c - 1) * C);
       store(h0, (c - 1) * C);
       break;
     }
-    cb = c * C;
-    r.step(h1, h0, c, get);
-    store(h0, (c - 1) * C);
+    if (c == 1)
+      r.step(h1, h0, c, get, none);
+    else
+      r.template step<true>(h1, h0, c, get, put);
     if ((c + 1) * C >= len) {
-      r.template bwd<false, true>(h1, h0, c * C);
+      store(h0, (c - 1) * C);
+      r.template bwd<false, GDM_MASS_EDGE_MODE>(h1, h0, c * C);
       store(h1, c * C);
       break;
     }
-    cb = (c + 1) * C;
-    r.step(h0, h1, c + 1, get);
-    store(h1, c * C);
+    r.template step<true>(h0, h1, c + 1, get, put);
   }
 }
 
@@ -568,11 +665,12 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
   GDM_WAIT_VMCNT(0);
   if (C < len) dma(tile1, C);
   open_row(tile0);
-  r.template fwd<true>(h0, h1, 0, get);
+  auto none = [](double) {};
+  r.template fwd<GDM_MASS_EDGE_MODE>(h0, h1, 0, get, none);
   for (int c = 1;; c += 2) {
     // ---- chunk c (odd): tile1, ring h1; chunk c - 1 in h0 (its input tile0 is free) ----
     if (c * C >= len) {
-      r.template bwd<false, true>(h0, h1, (c - 1) * C);
+      r.template bwd<false, GDM_MASS_EDGE_MODE>(h0, h1, (c - 1) * C);
       write_row(tile0, h0);
       store(tile0, (c - 1) * C);
       break;
@@ -583,12 +681,12 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
       GDM_WAIT_VMCNT(UPR);  // DMA(c) retired; the stores issued after it may be in flight
     if ((c + 1) * C < len) dma(tile0, (c + 1) * C);
     open_row(tile1);
-    r.step(h1, h0, c, get);
+    r.step(h1, h0, c, get, none);
     write_row(tile1, h0);
     store(tile1, (c - 1) * C);
     // ---- chunk c + 1 (even): tile0, ring h0; chunk c in h1 ----
     if ((c + 1) * C >= len) {
-      r.template bwd<false, true>(h1, h0, c * C);
+      r.template bwd<false, GDM_MASS_EDGE_MODE>(h1, h0, c * C);
       write_row(tile1, h1);
       store(tile1, c * C);
       break;
@@ -596,7 +694,7 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
     GDM_WAIT_VMCNT(UPR);
     if ((c + 2) * C < len) dma(tile1, (c + 2) * C);
     open_row(tile0);
-    r.step(h0, h1, c + 1, get);
+    r.step(h0, h1, c + 1, get, none);
     write_row(tile0, h1);
     store(tile0, c * C);
   }

@@ -17,7 +17,7 @@ for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursiv
         d = row.get("Dispatch_Id", row.get("Correlation_Id", "0"))
         vals[k][c][d] = vals[k][c].get(d, 0.0) + float(row.get("Counter_Value", 0))
 for k, cs in vals.items():
-    if "stencil" not in k and "face" not in k and "chol" not in k:
+    if not any(s in k for s in ("stencil", "face", "chol", "mass3")):
         continue
     print(k[:90])
     for c in sorted(cs):
