@@ -1830,4 +1830,85 @@ int gdm_time_op(gdm_op *op, int which, const double *src, double *dst, const dou
   GDM_GUARD_END
 }
 
+// ---- cut-cell systems (host assembly in gdm_cut.cpp) ----------------------
+struct gdm_cut_system;
+int gdmh_cut_poisson_create(int p, int n_sub, double lo, double hi, const double *center, double radius,
+                            int ghost_penalty, double rhs_value, double bc_value, gdm_cut_system **out, char *err,
+                            size_t err_len);
+void gdmh_cut_info(const gdm_cut_system *S, int64_t *n_rows, int64_t *nnz, int64_t *n_inside, int64_t *n_intersected);
+void gdmh_cut_arrays(const gdm_cut_system *S, const int64_t **row_ptr, const uint32_t **cols, const double **vals,
+                     const double **rhs);
+double gdmh_cut_l2_error(const gdm_cut_system *S, const double *u);
+void gdmh_cut_destroy(gdm_cut_system *S);
+
+int gdm_cut_poisson_create(int p, int n_sub, double lo, double hi, const double *center, double radius,
+                           int ghost_penalty, double rhs_value, double bc_value, gdm_cut_system **out) {
+  if (!out) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  char err[256] = {0};
+  if (gdmh_cut_poisson_create(p, n_sub, lo, hi, center, radius, ghost_penalty, rhs_value, bc_value, out, err,
+                              sizeof(err)) != 0)
+    return fail(std::strstr(err, "not implemented") ? GDM_ERR_UNSUPPORTED : GDM_ERR_ARG, err);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_poisson_info(const gdm_cut_system *S, int64_t *n_rows, int64_t *nnz, int64_t *n_inside_cells,
+                         int64_t *n_intersected_cells) {
+  if (!S || !n_rows || !nnz || !n_inside_cells || !n_intersected_cells) return fail(GDM_ERR_ARG, "NULL argument");
+  gdmh_cut_info(S, n_rows, nnz, n_inside_cells, n_intersected_cells);
+  return GDM_OK;
+}
+
+int gdm_cut_poisson_matrix(const gdm_cut_system *S, int device, gdm_csr **A) {
+  if (!S || !A) return fail(GDM_ERR_ARG, "NULL argument");
+  int64_t n, nnz, a, b;
+  gdmh_cut_info(S, &n, &nnz, &a, &b);
+  const int64_t *rp;
+  const uint32_t *ci;
+  const double *v, *r;
+  gdmh_cut_arrays(S, &rp, &ci, &v, &r);
+  return gdm_csr_create(device, n, n, nnz, rp, ci, v, 0, A);
+}
+
+int gdm_cut_poisson_csr(const gdm_cut_system *S, int64_t *row_ptr_host, uint32_t *cols_host, double *vals_host) {
+  if (!S || !row_ptr_host || !cols_host || !vals_host) return fail(GDM_ERR_ARG, "NULL argument");
+  int64_t n, nnz, a, b;
+  gdmh_cut_info(S, &n, &nnz, &a, &b);
+  const int64_t *rp;
+  const uint32_t *ci;
+  const double *v, *r;
+  gdmh_cut_arrays(S, &rp, &ci, &v, &r);
+  std::memcpy(row_ptr_host, rp, sizeof(int64_t) * (n + 1));
+  std::memcpy(cols_host, ci, sizeof(uint32_t) * nnz);
+  std::memcpy(vals_host, v, sizeof(double) * nnz);
+  return GDM_OK;
+}
+
+int gdm_cut_poisson_rhs(const gdm_cut_system *S, double *rhs_host) {
+  if (!S || !rhs_host) return fail(GDM_ERR_ARG, "NULL argument");
+  int64_t n, nnz, a, b;
+  gdmh_cut_info(S, &n, &nnz, &a, &b);
+  const int64_t *rp;
+  const uint32_t *ci;
+  const double *v, *r;
+  gdmh_cut_arrays(S, &rp, &ci, &v, &r);
+  std::memcpy(rhs_host, r, sizeof(double) * n);
+  return GDM_OK;
+}
+
+int gdm_cut_poisson_l2_error(const gdm_cut_system *S, const double *u_host, double *err) {
+  if (!S || !u_host || !err) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  *err = gdmh_cut_l2_error(S, u_host);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_poisson_destroy(gdm_cut_system *S) {
+  gdmh_cut_destroy(S);
+  return GDM_OK;
+}
+
 }  // extern "C"
+

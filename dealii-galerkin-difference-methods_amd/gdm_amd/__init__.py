@@ -7,8 +7,8 @@ operator classes.  No CPU fallback exists.
 """
 from ._capi import GdmError, load, declared_symbols, device_count  # noqa: F401
 from .operator import GdmOperator  # noqa: F401
-from .sparse import SparseMatrix, solve_cg  # noqa: F401
+from .sparse import CutPoisson, SparseMatrix, solve_cg  # noqa: F401
 from .problem import Advection01, AdvectionProblem, DiscreteTime, WaveProblem  # noqa: F401
 
-__all__ = ["GdmError", "GdmOperator", "SparseMatrix", "solve_cg", "load", "declared_symbols", "device_count",
+__all__ = ["GdmError", "GdmOperator", "SparseMatrix", "CutPoisson", "solve_cg", "load", "declared_symbols", "device_count",
            "Advection01", "AdvectionProblem", "WaveProblem", "DiscreteTime"]

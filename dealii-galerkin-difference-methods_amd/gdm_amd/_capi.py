@@ -136,6 +136,14 @@ def load():
         "gdm_csr_read_triplets": [i32, ctypes.c_char_p, i32, ctypes.POINTER(P)],
         "gdm_csr_write_triplets": [P, ctypes.c_char_p, i32],
         "gdm_csr_time_vmult": [P, P, P, i32, ctypes.POINTER(d)],
+        "gdm_cut_poisson_create": [i32, i32, d, d, P, d, i32, d, d, ctypes.POINTER(P)],
+        "gdm_cut_poisson_info": [P, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                 ctypes.POINTER(i64)],
+        "gdm_cut_poisson_matrix": [P, i32, ctypes.POINTER(P)],
+        "gdm_cut_poisson_csr": [P, P, P, P],
+        "gdm_cut_poisson_rhs": [P, P],
+        "gdm_cut_poisson_l2_error": [P, P, ctypes.POINTER(d)],
+        "gdm_cut_poisson_destroy": [P],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -191,3 +191,80 @@ def stencil_csr_2d(n, p, terms, device=0, rows_per_chunk=1 << 20):
         cols[s:e] = c.to(torch.int32)
         vals[s:e] = vv
     return row_ptr, cols, vals
+
+
+class CutPoisson:
+    """The 2D cut-cell Poisson system of prototypes/cut_poisson_01_gdm.cc
+    (`test<2>(ghost_penalty)`, :57-405): assembled on the host by
+    libgdm_hip.so (csrc/gdm_cut.cpp: MeshClassifier of the FE_Q(1) level set
+    of |x - center| - radius, the deal.II QuadratureGenerator (Saye) on every
+    intersected cell, (grad v, grad u)_inside + Nitsche + ghost penalty),
+    solved on the device:
+
+        S = CutPoisson(p=3, n_sub=64, ghost_penalty=True)
+        A = S.matrix()                      # SparseMatrix in HBM
+        x = torch.zeros(S.n_rows, ...); its, res = solve_cg(A, x, S.rhs_tensor(), "identity",
+                                                           S.n_rows, 1e-10, 1e-6)
+        S.l2_error(x)                       # the prototype's error line
+    """
+
+    def __init__(self, p=3, n_sub=64, lo=-1.21, hi=1.21, center=(0.0, 0.0), radius=1.0, ghost_penalty=False,
+                 rhs_value=4.0, bc_value=1.0):
+        self._lib = _capi.load()
+        self._h = ctypes.c_void_p()
+        c = (ctypes.c_double * 2)(*center)
+        check(self._lib.gdm_cut_poisson_create(int(p), int(n_sub), float(lo), float(hi), c, float(radius),
+                                               1 if ghost_penalty else 0, float(rhs_value), float(bc_value),
+                                               ctypes.byref(self._h)), "gdm_cut_poisson_create")
+        n, z, a, b = (ctypes.c_int64() for _ in range(4))
+        check(self._lib.gdm_cut_poisson_info(self._h, ctypes.byref(n), ctypes.byref(z), ctypes.byref(a),
+                                             ctypes.byref(b)), "gdm_cut_poisson_info")
+        self.n_rows, self.nnz, self.n_inside_cells, self.n_intersected_cells = n.value, z.value, a.value, b.value
+        self.h = (hi - lo) / n_sub
+
+    def close(self):
+        if self._h:
+            self._lib.gdm_cut_poisson_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def matrix(self, device=0):
+        """the system matrix as a device CSR (SparseMatrix)"""
+        h = ctypes.c_void_p()
+        check(self._lib.gdm_cut_poisson_matrix(self._h, int(device), ctypes.byref(h)), "gdm_cut_poisson_matrix")
+        A = SparseMatrix(None, None, None, device=device, _handle=h)
+        A.use_torch_stream()
+        return A
+
+    def csr(self):
+        """host copy (row_ptr int64, cols uint32, vals fp64) of the system matrix"""
+        rp = np.zeros(self.n_rows + 1, dtype=np.int64)
+        ci = np.zeros(self.nnz, dtype=np.uint32)
+        v = np.zeros(self.nnz)
+        check(self._lib.gdm_cut_poisson_csr(self._h, rp.ctypes.data_as(ctypes.c_void_p),
+                                            ci.ctypes.data_as(ctypes.c_void_p), v.ctypes.data_as(ctypes.c_void_p)),
+              "gdm_cut_poisson_csr")
+        return rp, ci, v
+
+    def rhs(self):
+        """right-hand side (host numpy array, global DoF order)"""
+        r = np.zeros(self.n_rows)
+        check(self._lib.gdm_cut_poisson_rhs(self._h, r.ctypes.data_as(ctypes.c_void_p)), "gdm_cut_poisson_rhs")
+        return r
+
+    def l2_error(self, u):
+        """L2 error of u (host array or device tensor) on the inside quadrature (:349-405)"""
+        if hasattr(u, "cpu"):
+            u = u.detach().cpu().numpy()
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        if u.size != self.n_rows:
+            raise GdmError("l2_error: %d values for %d DoFs" % (u.size, self.n_rows))
+        e = ctypes.c_double()
+        check(self._lib.gdm_cut_poisson_l2_error(self._h, u.ctypes.data_as(ctypes.c_void_p), ctypes.byref(e)),
+              "gdm_cut_poisson_l2_error")
+        return e.value

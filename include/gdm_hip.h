@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 5
+#define GDM_HIP_ABI_VERSION 6
 
 enum gdm_status {
   GDM_OK = 0,
@@ -361,6 +361,43 @@ int gdm_csr_read_triplets(int device, const char *path, int binary, gdm_csr **ou
 int gdm_csr_write_triplets(const gdm_csr *A, const char *path, int binary);
 /* mean time of n_iter back-to-back gdm_csr_vmult calls (HIP events, ms) */
 int gdm_csr_time_vmult(gdm_csr *A, const double *src, double *dst, int n_iter, double *avg_ms_host);
+
+/* ------------------------------------------------------------------------
+ * Cut-cell systems: the 2D cut Poisson problem of
+ * prototypes/cut_poisson_01_gdm.cc:57-405 assembled on the host
+ * (csrc/gdm_cut.cpp) and solved by the device SpMV + SolverCG above.
+ *
+ *   gdm_cut_poisson_create   the reference's test<2>(ghost_penalty) system:
+ *                            GDM degree p, n_sub^2 cells on [lo, hi]^2,
+ *                            level set = FE_Q(1) interpolant of
+ *                            |x - center| - radius (SignedDistance::Sphere),
+ *                            NonMatching::MeshClassifier, the deal.II
+ *                            QuadratureGenerator (Saye) on each intersected
+ *                            cell, (grad v, grad u)_inside + Nitsche
+ *                            (gamma = 5 (p+1) p) + ghost penalty (0.5 * 0.5 h
+ *                            [d_n v][d_n u]) if ghost_penalty, rhs
+ *                            rhs_value v + Nitsche data bc_value, zero
+ *                            diagonals -> 1 (:148-323).  2D only.
+ *   gdm_cut_poisson_matrix   the system matrix as a device CSR (gdm_csr_*)
+ *   gdm_cut_poisson_csr      host copy of the CSR arrays (caller-allocated,
+ *                            sizes from gdm_cut_poisson_info; ascending
+ *                            columns, the entries cell assembly touches plus
+ *                            every diagonal)
+ *   gdm_cut_poisson_rhs      the right-hand side (host copy, n_rows values)
+ *   gdm_cut_poisson_l2_error L2 error over the inside quadrature against the
+ *                            manufactured solution bc + rhs/4 (r^2 - |x-c|^2)
+ *                            (:349-405); u_host in the global DoF order
+ * ------------------------------------------------------------------------ */
+typedef struct gdm_cut_system gdm_cut_system;
+int gdm_cut_poisson_create(int p, int n_sub, double lo, double hi, const double *center /* [2] or NULL */,
+                           double radius, int ghost_penalty, double rhs_value, double bc_value, gdm_cut_system **out);
+int gdm_cut_poisson_info(const gdm_cut_system *S, int64_t *n_rows, int64_t *nnz, int64_t *n_inside_cells,
+                         int64_t *n_intersected_cells);
+int gdm_cut_poisson_matrix(const gdm_cut_system *S, int device, gdm_csr **A);
+int gdm_cut_poisson_csr(const gdm_cut_system *S, int64_t *row_ptr_host, uint32_t *cols_host, double *vals_host);
+int gdm_cut_poisson_rhs(const gdm_cut_system *S, double *rhs_host);
+int gdm_cut_poisson_l2_error(const gdm_cut_system *S, const double *u_host, double *err);
+int gdm_cut_poisson_destroy(gdm_cut_system *S);
 
 #ifdef __cplusplus
 }

@@ -269,3 +269,27 @@ def test_cut_poisson_01_device_cg_golden(ghost_penalty):
     assert abs(e - golden) / golden < 1.5e-4, e
     assert abs(its - its_ref) <= (5 if ghost_penalty else 20), (its, its_ref)
     assert res <= 1e-6 * np.linalg.norm(rhs)
+
+
+def test_cut_poisson_library_device_cg_golden():
+    """The product path end to end: the library's own cut-cell assembly
+    (gdm_amd.CutPoisson = csrc/gdm_cut.cpp, ghost penalty) -> device CSR ->
+    device SolverCG(identity, ReductionControl(n, 1e-10, 1e-6)) -> the
+    library's L2 error reproduces prototypes/cut_poisson_01_gdm.output
+    (4.3420e-04, to the 1.5e-4 fp64-order spread of the unconverged iterate)."""
+    import gdm_amd
+
+    S = gdm_amd.CutPoisson(3, 64, ghost_penalty=True)
+    A = S.matrix()
+    assert A.m() == S.n_rows and A.n_nonzero_elements() == S.nnz
+    x = torch.zeros(S.n_rows, dtype=torch.float64, device="cuda")
+    b = dev(S.rhs())
+    its, res = gdm_amd.solve_cg(A, x, b, "identity", S.n_rows, 1e-10, 1e-6)
+    e = S.l2_error(x)
+    assert abs(e - 4.3420e-04) / 4.3420e-04 < 1.5e-4, (e, its)
+    # SpMV of the device CSR against the host CSR
+    rp, c, v = S.csr()
+    u = np.random.default_rng(5).uniform(-1, 1, S.n_rows)
+    y = torch.zeros(S.n_rows, dtype=torch.float64, device="cuda")
+    A.vmult(y, dev(u))
+    assert rel(host(y), O.csr_vmult(rp, c.astype(np.int64), v, u)) < RTOL_SPMV
