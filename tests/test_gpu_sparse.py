@@ -247,9 +247,9 @@ def test_cut_poisson_01_device_cg_golden(ghost_penalty):
     restatement oracle/cut2d.py, pinned to the same golden on the CPU) solved
     by the device SpMV + SolverCG (identity, ReductionControl(n, 1e-10,
     1e-6), :326-335): the L2 error of the device solution reproduces
-    prototypes/cut_poisson_01_gdm.output to 1.5e-4 relative, the spread of
-    the (unconverged, rel 1e-6) CG iterate's error under fp64 summation
-    order (see tests/test_cut2d_golden.py)."""
+    prototypes/cut_poisson_01_gdm.output to the spread of the (unconverged,
+    rel 1e-6) CG iterate's error under fp64 summation order: 1.5e-4 with
+    ghost penalty, 1 % without (see tests/test_cut_assembly.py)."""
     import cut2d
 
     sp = _sp()
@@ -262,12 +262,14 @@ def test_cut_poisson_01_device_cg_golden(ghost_penalty):
     its, res = sp.solve_cg(A, x, dev(rhs), preconditioner="identity", max_it=n, abs_tol=1e-10, rel_tol=1e-6)
     e = P.l2_error(host(x))
     golden = 4.3420e-04 if ghost_penalty else 4.2303e-04
-    # the device sums in another order than deal.II / the oracle: the printed
-    # last digit of the CG iterate's error moves by one (4.34198e-04 oracle,
-    # 4.34205e-04 device and numpy-pairwise; 4.2301 / 4.2303 / 4.2304e-04
-    # without ghost penalty)
-    assert abs(e - golden) / golden < 1.5e-4, e
-    assert abs(its - its_ref) <= (5 if ghost_penalty else 20), (its, its_ref)
+    # the device sums in another order than deal.II / the oracle: with ghost
+    # penalty the printed last digit of the CG iterate's error moves by one
+    # (4.34198e-04 oracle, 4.34205e-04 device); without, the unstabilised
+    # system's unconverged iterate moves by up to 1 % (4.2301 / 4.2303 / 4.2594 /
+    # 4.2631e-04 for four summation orders, converged 4.2918e-04)
+    assert abs(e - golden) / golden < (1.5e-4 if ghost_penalty else 1e-2), e
+    # (without ghost penalty the iteration count moves with the order as well: 595 oracle, 663 row-block SpMV)
+    assert abs(its - its_ref) <= (5 if ghost_penalty else its_ref // 5), (its, its_ref)
     assert res <= 1e-6 * np.linalg.norm(rhs)
 
 
