@@ -222,7 +222,9 @@ __global__ void __launch_bounds__(CSR_BLOCK) cg_dir_kernel(int64_t n, const doub
 }
 
 // iteration it: x += alpha p ; r -= alpha q with alpha = gh(it - 1) / p.Ap ;
-// partials of r.r and r.z
+// partials of r.r and r.z.  Grid-stride over a fixed grid (CG_GRID blocks at
+// most): few partials for cg_reduce_kernel, a fixed summation order.
+constexpr int CG_GRID = 2048;
 __global__ void __launch_bounds__(CSR_BLOCK) cg_update_kernel(int64_t n, double *__restrict__ x,
                                                               double *__restrict__ r, const double *__restrict__ p,
                                                               const double *__restrict__ q,
@@ -230,15 +232,14 @@ __global__ void __launch_bounds__(CSR_BLOCK) cg_update_kernel(int64_t n, double 
                                                               const double *__restrict__ S, int it,
                                                               double *__restrict__ part, int64_t nparts) {
   __shared__ double sh[CSR_BLOCK / 64];
-  const int64_t i = (int64_t)blockIdx.x * CSR_BLOCK + threadIdx.x;
   double rr = 0.0, rz = 0.0;
-  if (i < n) {
-    const double alpha = S[S_GH + ((it - 1) & 1)] / S[S_PAP];
+  const double alpha = S[S_GH + ((it - 1) & 1)] / S[S_PAP];
+  for (int64_t i = (int64_t)blockIdx.x * CSR_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * CSR_BLOCK) {
     x[i] += alpha * p[i];
     const double ri = r[i] - alpha * q[i];
     r[i] = ri;
-    rr = ri * ri;
-    rz = dinv ? ri * dinv[i] * ri : rr;
+    rr += ri * ri;
+    rz += dinv ? ri * dinv[i] * ri : ri * ri;
   }
   const double a = block_sum(rr, sh);
   __syncthreads();
@@ -247,6 +248,17 @@ __global__ void __launch_bounds__(CSR_BLOCK) cg_update_kernel(int64_t n, double 
     part[blockIdx.x] = a;
     part[nparts + blockIdx.x] = c;
   }
+}
+
+// partials of p.q (q = A p), grid-stride like cg_update_kernel
+__global__ void __launch_bounds__(CSR_BLOCK) cg_pap_kernel(int64_t n, const double *__restrict__ p,
+                                                           const double *__restrict__ q, double *__restrict__ part) {
+  __shared__ double sh[CSR_BLOCK / 64];
+  double d = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * CSR_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * CSR_BLOCK)
+    d += p[i] * q[i];
+  const double t = block_sum(d, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
 }
 
 // structural checks of a device CSR: row_ptr non-decreasing, cols < n_cols;
@@ -657,13 +669,19 @@ int gdm_csr_cg(gdm_csr *A, const double *b, double *x, int precond, int max_it, 
     bool converged = res <= tol;
     CgTrace trace;
     trace.init(A);
+    // p.Ap and r.r / r.z from grid-stride kernels over gs <= CG_GRID blocks
+    // (the per-row-block SpMV partials and one partial per 256 rows made the
+    // single-block reductions 100 us each at config 5)
+    const unsigned gs = (unsigned)std::min<int64_t>(CG_GRID, cdiv(n, CSR_BLOCK));
+    (void)ns;
     while (!converged && its < max_it) {
       ++its;
       cg_dir_kernel<<<gv, CSR_BLOCK, 0, A->stream>>>(n, A->r, dinv, A->p, A->S, its);
-      hip_check(launch_spmv(A, A->p, nullptr, A->q, A->part), "spmv launch");
-      cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, ns, 1, S_PAP, S_PAP, A->S);
-      cg_update_kernel<<<gv, CSR_BLOCK, 0, A->stream>>>(n, x, A->r, A->p, A->q, dinv, A->S, its, A->part, gv);
-      cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, gv, 2, S_RR, S_GH + (its & 1), A->S);
+      hip_check(launch_spmv(A, A->p, nullptr, A->q, nullptr), "spmv launch");
+      cg_pap_kernel<<<gs, CSR_BLOCK, 0, A->stream>>>(n, A->p, A->q, A->part);
+      cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, gs, 1, S_PAP, S_PAP, A->S);
+      cg_update_kernel<<<gs, CSR_BLOCK, 0, A->stream>>>(n, x, A->r, A->p, A->q, dinv, A->S, its, A->part, gs);
+      cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, gs, 2, S_RR, S_GH + (its & 1), A->S);
       hip_check(hipGetLastError(), "cg iteration");
       if (its <= 40) trace.step(A, x, its);
       res = std::sqrt(read_scalar(A, S_RR));

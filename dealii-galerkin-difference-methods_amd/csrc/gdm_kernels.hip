@@ -42,6 +42,11 @@ namespace gdmk {
 #else
 #define GDM_DBG(a, bit) false
 #endif
+// v8 handoff: 0 = one (A, B) plane, barriers F / L per plane, 3-slot DMA
+// ring; 1 = two (A, B) planes, one barrier per plane, 2-slot DMA ring
+#ifndef GDM_STENCIL_DB
+#define GDM_STENCIL_DB 1
+#endif
 #define GDM_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
 // Coefficient tables are read-only for the whole launch and indexed by
@@ -552,11 +557,18 @@ struct Geom8 {
   // ring depth that fits that LDS share (3 slots if possible, else 2)
   static constexpr int WGS = NW <= 12 ? 2 : 1;
   static constexpr size_t LDS_CAP = (160 * 1024) / WGS;
+#if GDM_STENCIL_DB
+  // double-buffered (A, B) planes, 2-slot DMA ring
+  static constexpr int NSLOT = 2;
+  static constexpr int NABUF = 2;
+#else
   static constexpr int NSLOT =
       sizeof(double) * (size_t)(3 * USZ + ABSZ + ZTSZ + YCSZ + CORRSZ + (P + 1) * TX * NAB) <= LDS_CAP ? 3 : 2;
+  static constexpr int NABUF = 1;
+#endif
   static constexpr int YWSZ = (P + 1) * TX * NAB;  // y-wall corrections of one plane
   static constexpr int OFF_AB = NSLOT * USZ;
-  static constexpr int OFF_ZT = OFF_AB + ABSZ;
+  static constexpr int OFF_ZT = OFF_AB + NABUF * ABSZ;
   static constexpr int OFF_YC = OFF_ZT + ZTSZ;
   static constexpr int OFF_CORR = OFF_YC + YCSZ;
   static constexpr int OFF_YW = OFF_CORR + CORRSZ;
@@ -773,6 +785,52 @@ __device__ __forceinline__ void ywall8(const StencilArgs &a, const Tile7 &t) {
 template <int P, int R, int NC, int NP, int BK, int CH>
 __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) {
   using G = Geom8<P, R, NC, NP, BK>;
+#if GDM_STENCIL_DB
+  // plane i: X(i) straight into (A, B) buffer i & 1 | B_i | [y walls: ywall(i) | M_i] | DMA(i + 2)
+  // (the buffer was last read by the consumers' Y(i - 2), before they reached B_(i-1))
+  {
+    ldouble *u[2] = {t.u0, t.u0 + G::USZ};
+    const int n = t.ze - t.zs;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (k < n) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + k, u[k]);
+    GDM_LDS_BARRIER();  // tables in LDS
+    dpair V1[4];
+    XWallPre<P, BK> xpre;
+    if (t.ncw > 0) xwall8_pre<P, R, NC, NP, BK>(a, t, xpre);
+    for (int i = 0; i < n; ++i) {
+      const int slot = i & 1;
+      if (GDM_DBG(a, 8))
+        ;
+      else if (i + 1 < n)
+        wait_dma_planes<0, 1, P, R, NC, NP, BK, CH>(t.wv);
+      else
+        GDM_WAIT_VMCNT(0);
+      Tile7 tt = t;
+      tt.ab0 = t.ab0 + slot * G::ABSZ;
+#pragma unroll
+      for (int ps = 0; ps < G::NPASS; ++ps) {
+        const int g = t.wv + ps * NP;
+        if (g < G::NG) {
+          if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, tt, u[slot], g, V1);
+          write_ab8<P, R, NC, NP, BK>(tt, g, V1);
+          if (t.ncw > 0) {
+            XWall<P, BK> xw0;
+            xwall8_calc<P, R, NC, NP, BK>(tt, u[slot], g, xpre, xw0);
+            xwall8_add<P, BK>(tt, xw0);
+          }
+        }
+      }
+      GDM_LDS_BARRIER();  // B_i: AB(i) complete
+      if (t.yedge) {
+        ywall8<P, R, NC, NP, BK>(a, tt);
+        GDM_LDS_BARRIER();  // M_i
+      }
+      if (i + 2 < n && !GDM_DBG(a, 8)) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot]);
+    }
+    return;
+  }
+#endif
   constexpr int NS = G::NSLOT;
   ldouble *u[3] = {t.u0, t.u0 + G::USZ, t.u0 + (NS > 2 ? 2 : 0) * G::USZ};
   const int n = t.ze - t.zs;
@@ -897,12 +955,18 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
   constexpr int W = G::W;
   if (zz < t.ze) {
     double D[R], E[R];
-    GDM_LDS_BARRIER();  // L_i
+    GDM_LDS_BARRIER();  // L_i (DB: B_i)
+#if GDM_STENCIL_DB
+    Tile7 tt = t;
+    tt.ab0 = t.ab0 + ((zz - t.zs) & 1) * G::ABSZ;
+#else
+    const Tile7 &tt = t;
+#endif
     if (GDM_DBG(a, 1)) {
 #pragma unroll
       for (int j = 0; j < R; ++j) D[j] = E[j] = (double)zz;
     } else {
-      ysweep8<P, R, NC, NP, BK, PF>(a, t, D, E);
+      ysweep8<P, R, NC, NP, BK, PF>(a, tt, D, E);
     }
     if constexpr (YW) {
       GDM_LDS_BARRIER();  // M_i
@@ -921,7 +985,9 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
         }
       }
     }
+#if !GDM_STENCIL_DB
     GDM_LDS_BARRIER();  // F_i+1
+#endif
     if (!GDM_DBG(a, 2)) {
       if constexpr (!WALL) {
         // interior z column: out += mhat[k] E + zd[k] D with zd = dint dhat[2p - k]
@@ -1023,7 +1089,9 @@ __device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
   GDM_LDS_BARRIER();  // tables in LDS
+#if !GDM_STENCIL_DB
   GDM_LDS_BARRIER();  // F_0
+#endif
   // ZI: the host launched this kernel only on output planes whose z columns
   // are all interior -> compile-time z bands, no table reads; otherwise every
   // plane reads its column (wall columns or the interior one) from LDS
@@ -1049,6 +1117,7 @@ template <int P, int R, int NC, int NP, int BK, int CH, int PF, bool ZI>
 __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, NP, BK>::WGS) / 4)
     stencil8_kernel(StencilArgs a) {
   using G = Geom8<P, R, NC, NP, BK>;
+  static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget of one workgroup per CU");
   extern __shared__ __attribute__((aligned(16))) double smem[];
   ldouble *lds = (ldouble *)smem;
   Tile7 t;

@@ -1,7 +1,7 @@
 # round-end rehearsal: smoke, the whole GPU suite, the default bench line, rocprof kernel stats of the bench, C5 cut solve
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/final; mkdir -p $OUT
+OUT=${OUT:-gpurun_out/final}; mkdir -p $OUT
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?; echo smoke rc=$rc; tail -n 1 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; echo gpu rc=$rc; tail -n 2 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err; rc=$?; echo bench rc=$rc; cut -c1-300 $OUT/bench.json; [ $rc -eq 0 ] || exit $rc
