@@ -188,6 +188,67 @@ __device__ __forceinline__ void stage_group7(const StencilArgs &a, const Tile7 &
   }
 }
 
+// plane-invariant per-lane DMA byte offsets of this producer wave's row groups
+// (the plane is selected by the buffer resource alone): computed once per
+// tile instead of ~15 VALU + ~15 SALU per DMA instruction and plane;
+// 0xffffffff = the lane issues nothing for that instruction
+template <int P, int R, int NC, int NP, int BK, int CH>
+struct DmaPre7 {
+  uint32_t vo[Geom7<P, R, NC, NP, BK>::NPASS][Dma7<P, R, NC, NP, BK, CH>::NI_FULL];
+};
+
+template <int P, int R, int NC, int NP, int BK, int CH>
+__device__ __forceinline__ void stage_pre7(const StencilArgs &a, const Tile7 &t, DmaPre7<P, R, NC, NP, BK, CH> &d) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  using S = Dma7<P, R, NC, NP, BK, CH>;
+#pragma unroll
+  for (int ps = 0; ps < G::NPASS; ++ps) {
+    const int g = t.wv + ps * NP;
+    const bool last = g == G::NG - 1;
+    const int nch = (last ? S::ROWS_LAST : 4) * S::CPR;
+#pragma unroll
+    for (int i = 0; i < S::NI_FULL; ++i) {
+      const int e = i * 64 + t.lane;
+      const int rr = e / S::CPR, c = e - rr * S::CPR;
+      const int gy = t.y0 - P + 4 * g + rr;
+      const int gx2 = (t.x0 - G::XH) * 2 + c * S::DPC;
+      uint32_t voff = 0x80000000u;  // out of range -> zeros
+      if (gy >= a.in_y0 && gy < a.in_y1 && gx2 >= 0 && gx2 < 2 * a.Nx)
+        voff = (uint32_t)(((int64_t)(gy - a.in_y0) * a.Nx * 2 + gx2) * 4);
+      d.vo[ps][i] = (g < G::NG && e < nch) ? voff : 0xffffffffu;
+    }
+  }
+}
+
+template <int P, int R, int NC, int NP, int BK, int CH>
+__device__ __forceinline__ void stage_plane_pre7(const StencilArgs &a, const Tile7 &t, int zz, ldouble *ubuf,
+                                                 const DmaPre7<P, R, NC, NP, BK, CH> &d) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  using S = Dma7<P, R, NC, NP, BK, CH>;
+  const int ny_in = a.in_y1 - a.in_y0;
+  const double *plane = a.src + (int64_t)(zz - a.in_z0) * ny_in * a.Nx;
+  const int nbytes = (int)((int64_t)ny_in * a.Nx * 8);
+  __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)plane, 0, nbytes, 0x00020000);
+#pragma unroll
+  for (int ps = 0; ps < G::NPASS; ++ps) {
+    const int g = t.wv + ps * NP;
+    if (g < G::NG) {
+      const int ni = g == G::NG - 1 ? S::NI_LAST : S::NI_FULL;  // wave-uniform: the count wait_dma_planes expects
+      auto *gbase = (__attribute__((address_space(3))) char *)(ubuf + g * 4 * G::RL);
+#pragma unroll
+      for (int i = 0; i < S::NI_FULL; ++i) {
+        if (i < ni && d.vo[ps][i] != 0xffffffffu) {
+          auto *dst = (__attribute__((address_space(3))) void *)(gbase + i * 64 * CH);
+          if constexpr (CH == 16)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, d.vo[ps][i], 0, 0, 0);
+          else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, d.vo[ps][i], 0, 0, 0);
+        }
+      }
+    }
+  }
+}
+
 template <int P, int R, int NC, int NP, int BK, int CH>
 __device__ __forceinline__ void stage_plane7(const StencilArgs &a, const Tile7 &t, int zz, ldouble *ubuf) {
   using G = Geom7<P, R, NC, NP, BK>;
@@ -791,9 +852,11 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
   {
     ldouble *u[2] = {t.u0, t.u0 + G::USZ};
     const int n = t.ze - t.zs;
+    DmaPre7<P, R, NC, NP, BK, CH> dpre;
+    stage_pre7<P, R, NC, NP, BK, CH>(a, t, dpre);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
-      if (k < n) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + k, u[k]);
+      if (k < n) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + k, u[k], dpre);
     GDM_LDS_BARRIER();  // tables in LDS
     dpair V1[4];
     XWallPre<P, BK> xpre;
@@ -826,7 +889,7 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
         ywall8<P, R, NC, NP, BK>(a, tt);
         GDM_LDS_BARRIER();  // M_i
       }
-      if (i + 2 < n && !GDM_DBG(a, 8)) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot]);
+      if (i + 2 < n && !GDM_DBG(a, 8)) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre);
     }
     return;
   }

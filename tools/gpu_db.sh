@@ -2,7 +2,7 @@
 export TMPDIR=/tmp
 OUT=gpurun_out/db; mkdir -p $OUT
 L=$PWD/dealii-galerkin-difference-methods_amd/lib/variants
-export GDM_HIP_LIB=$L/db/libgdm_hip.so
+export GDM_HIP_LIB=$L/${VAR:-db}/libgdm_hip.so
 timeout -k 10 150 python -u -c "
 import sys, numpy as np, torch
 sys.path[:0] = ['dealii-galerkin-difference-methods_amd', 'oracle']
@@ -18,13 +18,13 @@ ref = m.kron_apply([(B[0], M[1], M[2]), (M[0], B[1], M[2]), (M[0], M[1], B[2])],
 y = op.new_vector(local=False)
 op.apply(torch.from_numpy(u).cuda(), y)
 torch.cuda.synchronize()
-print('db quick check rel err %.3e' % (np.linalg.norm(y.cpu().numpy() - ref) / np.linalg.norm(ref)))
+print('quick check rel err %.3e' % (np.linalg.norm(y.cpu().numpy() - ref) / np.linalg.norm(ref)))
 " > $OUT/quick.log 2>&1; rc=$?; cat $OUT/quick.log | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "advection and 5" > $OUT/pt.log 2>&1; rc=$?; echo "db parity rc=$rc $(tail -n 1 $OUT/pt.log)"; [ $rc -le 1 ] || exit $rc
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "advection_apply_vs_cell_loop and a0-3-5 or v8" > $OUT/pt.log 2>&1; rc=$?; echo "db parity rc=$rc $(tail -n 1 $OUT/pt.log)"; [ $rc -le 1 ] || exit $rc
 ops() { timeout -k 10 120 python -u tools/bench_ops.py --configs C3 --ops apply --iters 30 2>/dev/null | python3 -c "import sys,json
 for l in sys.stdin:
   d=json.loads(l); print('%.4f ms' % d['ms'])"; }
-for v in db main db main; do
+for v in ${VAR:-db} main ${VAR:-db} main; do
   if [ $v = main ]; then unset GDM_HIP_LIB; else export GDM_HIP_LIB=$L/$v/libgdm_hip.so; fi
   echo "== stencil $v $(ops)" || exit 1
 done
