@@ -884,12 +884,16 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
           }
         }
       }
+      // DMA(i + 2) into this wave's own rows of slot i & 1 as soon as its own
+      // reads of them have returned (before B_i: the barrier wait then
+      // overlaps the fetch)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (i + 2 < n && !GDM_DBG(a, 8)) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre);
       GDM_LDS_BARRIER();  // B_i: AB(i) complete
       if (t.yedge) {
         ywall8<P, R, NC, NP, BK>(a, tt);
         GDM_LDS_BARRIER();  // M_i
       }
-      if (i + 2 < n && !GDM_DBG(a, 8)) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre);
     }
     return;
   }
