@@ -1897,6 +1897,42 @@ int gdm_cut_poisson_rhs(const gdm_cut_system *S, double *rhs_host) {
   return GDM_OK;
 }
 
+int gdm_cut_poisson_solve(const gdm_cut_system *S, gdm_csr *A, double rel_tol, double abs_tol, int max_it,
+                          double *u_host, int *its_host, double *res_host) {
+  if (!S || !A || !u_host) return fail(GDM_ERR_ARG, "NULL argument");
+  int64_t n, nnz, a, b, m, mc, mz;
+  gdmh_cut_info(S, &n, &nnz, &a, &b);
+  if (gdm_csr_info(A, &m, &mc, &mz) != GDM_OK || m != n || mc != n) return fail(GDM_ERR_ARG, "matrix does not match the system");
+  GDM_GUARD_BEGIN
+  const int64_t *rp;
+  const uint32_t *ci;
+  const double *v, *r;
+  gdmh_cut_arrays(S, &rp, &ci, &v, &r);
+  double *bd = nullptr, *xd = nullptr;
+  hip_check(hipMalloc(&bd, sizeof(double) * std::max<int64_t>(n, 1)), "hipMalloc rhs");
+  if (hipMalloc(&xd, sizeof(double) * std::max<int64_t>(n, 1)) != hipSuccess) {
+    (void)hipFree(bd);
+    throw HipError("hipMalloc solution");
+  }
+  int rc = GDM_OK;
+  try {
+    hip_check(hipMemcpy(bd, r, sizeof(double) * n, hipMemcpyHostToDevice), "h2d rhs");
+    hip_check(hipMemset(xd, 0, sizeof(double) * n), "memset");
+    hip_check(hipDeviceSynchronize(), "sync");
+    rc = gdm_csr_cg(A, bd, xd, 0, max_it, abs_tol, rel_tol, its_host, res_host);
+    hip_check(hipDeviceSynchronize(), "sync");
+    hip_check(hipMemcpy(u_host, xd, sizeof(double) * n, hipMemcpyDeviceToHost), "d2h solution");
+  } catch (...) {
+    (void)hipFree(bd);
+    (void)hipFree(xd);
+    throw;
+  }
+  (void)hipFree(bd);
+  (void)hipFree(xd);
+  return rc;
+  GDM_GUARD_END
+}
+
 int gdm_cut_poisson_l2_error(const gdm_cut_system *S, const double *u_host, double *err) {
   if (!S || !u_host || !err) return fail(GDM_ERR_ARG, "NULL argument");
   GDM_GUARD_BEGIN

@@ -142,6 +142,7 @@ def load():
         "gdm_cut_poisson_matrix": [P, i32, ctypes.POINTER(P)],
         "gdm_cut_poisson_csr": [P, P, P, P],
         "gdm_cut_poisson_rhs": [P, P],
+        "gdm_cut_poisson_solve": [P, P, d, d, i32, P, ctypes.POINTER(i32), ctypes.POINTER(d)],
         "gdm_cut_poisson_l2_error": [P, P, ctypes.POINTER(d)],
         "gdm_cut_poisson_destroy": [P],
     }

@@ -384,6 +384,11 @@ int gdm_csr_time_vmult(gdm_csr *A, const double *src, double *dst, int n_iter, d
  *                            columns, the entries cell assembly touches plus
  *                            every diagonal)
  *   gdm_cut_poisson_rhs      the right-hand side (host copy, n_rows values)
+ *   gdm_cut_poisson_solve    SolverCG<>(ReductionControl(max_it, abs_tol,
+ *                            rel_tol)).solve(A, u, rhs, PreconditionIdentity())
+ *                            from u = 0 on the device (:332-335); A from
+ *                            gdm_cut_poisson_matrix; u_host receives the
+ *                            solution; GDM_ERR_STATE when max_it is reached
  *   gdm_cut_poisson_l2_error L2 error over the inside quadrature against the
  *                            manufactured solution bc + rhs/4 (r^2 - |x-c|^2)
  *                            (:349-405); u_host in the global DoF order
@@ -396,6 +401,8 @@ int gdm_cut_poisson_info(const gdm_cut_system *S, int64_t *n_rows, int64_t *nnz,
 int gdm_cut_poisson_matrix(const gdm_cut_system *S, int device, gdm_csr **A);
 int gdm_cut_poisson_csr(const gdm_cut_system *S, int64_t *row_ptr_host, uint32_t *cols_host, double *vals_host);
 int gdm_cut_poisson_rhs(const gdm_cut_system *S, double *rhs_host);
+int gdm_cut_poisson_solve(const gdm_cut_system *S, gdm_csr *A, double rel_tol, double abs_tol, int max_it,
+                          double *u_host, int *its_host, double *res_host);
 int gdm_cut_poisson_l2_error(const gdm_cut_system *S, const double *u_host, double *err);
 int gdm_cut_poisson_destroy(gdm_cut_system *S);
 

@@ -180,3 +180,33 @@ def test_driver_multirank_matches_single_rank(tmp_path, dim, p, n, steps, n_rank
     e1 = [float(v) for v in r1.stdout.strip().splitlines()[-1].split()[2:]]
     en = [float(v) for v in r.stdout.strip().splitlines()[-1].split()[2:]]
     np.testing.assert_allclose(en, e1, rtol=1e-7)
+
+
+CUT_APP = os.path.join(ROOT, "dealii-galerkin-difference-methods_amd", "lib", "host", "cut_poisson_app")
+
+
+def test_cut_poisson_driver_is_built():
+    assert os.access(CUT_APP, os.X_OK)
+
+
+@pytest.mark.gpu
+def test_cut_poisson_driver_reproduces_reference_output():
+    """cut_poisson_app = prototypes/cut_poisson_01_gdm.cc's main over the C
+    ABI (library cut assembly, device SolverCG, library L2 error) prints the
+    reference's two convergence tables; compared with
+    prototypes/cut_poisson_01_gdm.output: same layout, same mesh size, L2
+    errors to the fp64-order spread of the unconverged CG iterates (ghost
+    penalty 1.5e-4, without 1 %; tests/test_cut_assembly.py)."""
+    import json
+
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_outputs.json")))["cut_poisson_01"]["text"]
+    out = subprocess.run([CUT_APP], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()
+    assert [l for l in lines if l.startswith("Mesh")] == [l for l in ref if l.startswith("Mesh")]
+    got = [l.split() for l in lines if l.strip() and not l.startswith("Mesh")]
+    exp = [l.split() for l in ref if l.strip() and not l.startswith("Mesh")]
+    assert len(got) == len(exp) == 2
+    for (h, e), (hr, er), tol in zip(got, exp, (1e-2, 1.5e-4)):
+        assert h == hr
+        assert abs(float(e) - float(er)) / float(er) < tol, (e, er)
