@@ -51,22 +51,56 @@ def parse():
     ap.add_argument("--cpu-cells", type=int, default=24, help="cells per direction of the CPU-baseline sample")
     ap.add_argument("--pmc", default=os.environ.get("GDM_BENCH_PMC", "1"), help="collect HBM PMC traffic (1/0)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--metric-only", action="store_true",
+                    help="time only the metric's compute_rhs (no mass / RK-stage / PMC / CPU legs): for per-config "
+                         "rocprof kernel statistics")
     return ap.parse_args()
 
 
+def _band_csr(O, mesh, d, which):
+    """scipy CSR of the oracle's 1D band matrix (0 = M, 1 = C, 2 = L) along d"""
+    import scipy.sparse as sps
+
+    band = mesh.matrices_1d(d)[which]
+    N, p = band.shape[0], mesh.p
+    return sps.diags([band[max(0, -k + p):N - max(0, k - p) + max(0, -k + p), k][: N - abs(k - p)]
+                      for k in range(2 * p + 1)], [k - p for k in range(2 * p + 1)], shape=(N, N))
+
+
+def _timed(fn, budget):
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        fn()
+        reps += 1
+        if time.perf_counter() - t0 > budget:
+            break
+    return (time.perf_counter() - t0) / reps, reps
+
+
 def cpu_baseline(p, n_cells, threads):
-    """Reference algorithm (per-cell FEValues loop of stiffness.h:345-532) from
-    the CPU restatement in oracle/, on a bounded sample: `threads` host
-    threads, each running the cell loop over its own z-slab of cells into a
-    private vector (ctypes releases the GIL; the reference's MPI ranks do the
-    same with one slab each), summed; plus the 1-thread rate and the mass
-    solve the reference runs per stage (CSR mass + SolverCG with
-    PreconditionJacobi to rel 1e-14, advection/problem.h:236-267) at 24^3
-    cells."""
+    """Reference algorithms from the CPU restatement in oracle/ (test
+    infrastructure, the checker -- never the measured product), on bounded
+    samples of the benchmark's workloads:
+
+    * C3 (the metric): the per-cell FEValues loop of advection/stiffness.h:
+      345-532 on n_cells^3 cells; `threads` host threads, each running the cell
+      loop over its own z-slab of cells into a private vector (ctypes releases
+      the GIL; the reference's MPI ranks do the same with one slab each),
+      summed; plus the 1-thread rate;
+    * the per-stage mass solve of advection/problem.h:236-267 (CSR mass +
+      SolverCG/Jacobi to rel 1e-14) at 24^3 cells, 1 thread;
+    * C4: the wave stiffness cell loop of wave/stiffness.h:151-181 (p=7, 3D)
+      on z-slabs over `threads` threads;
+    * C5: cut_poisson_01_gdm.cc:332-335's SolverCG + PreconditionIdentity
+      iterations over a CSR with the full (2p+1)^2 GDM sparsity of
+      system.h:586-599 (the uncut Laplacian L(x)M + M(x)L, p=3), 1 thread.
+    """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from concurrent.futures import ThreadPoolExecutor
 
     import numpy as np
+    import scipy.sparse as sps
     import oracle as O
 
     a = (1.0, 0.15, -0.05)
@@ -83,36 +117,31 @@ def cpu_baseline(p, n_cells, threads):
         outs[t][:] = 0.0
         m.advection_rhs(a, u, bcs[t], cb=cb, ce=ce, rhs=outs[t])
 
-    def timed(fn, budget):
-        t0 = time.perf_counter()
-        reps = 0
-        while True:
-            fn()
-            reps += 1
-            if time.perf_counter() - t0 > budget:
-                break
-        return (time.perf_counter() - t0) / reps, reps
+    # C4 sample: wave p=7 cell loop, z-slabs over the same threads
+    nw = 12
+    mw = O.Mesh(3, 7, nw, -1.21, 1.21)
+    uw = np.random.default_rng(5).uniform(-1, 1, mw.n_dofs)
+    wb = [(nw * t // threads, nw * (t + 1) // threads) for t in range(threads)]
+
+    def wpart(t):
+        cb, ce = wb[t]
+        if ce > cb:
+            mw.wave_rhs(uw, impl=True, cb=cb, ce=ce)
 
     with ThreadPoolExecutor(threads) as ex:
         def all_parts():
             list(ex.map(part, range(threads)))
             np.sum(outs, axis=0)
 
-        dt_n, reps_n = timed(all_parts, 10.0)
+        dt_n, reps_n = _timed(all_parts, 10.0)
+        dt_w, reps_w = _timed(lambda: list(ex.map(wpart, range(threads))), 5.0)
     bc1 = np.random.default_rng(3).uniform(-1, 1, m.n_boundary_points())
-    dt_1, reps_1 = timed(lambda: m.advection_rhs(a, u, bc1), 5.0)
+    dt_1, reps_1 = _timed(lambda: m.advection_rhs(a, u, bc1), 5.0)
     # mass solve: CSR + CG(Jacobi) to rel 1e-14 (the reference's per-stage solve).  The CSR matrix is
     # the Kronecker product of the oracle's 1D mass matrices (equal to the cell-assembled matrix up to
     # round-off; the oracle's cell assembly itself takes minutes at this size)
-    import scipy.sparse as sps
-
     mm = O.Mesh(3, p, 24, 0.0, 1.0)
-    M1 = []
-    for d in range(3):
-        band = mm.matrices_1d(d)[0]
-        N = band.shape[0]
-        M1.append(sps.diags([band[max(0, -k + p):N - max(0, k - p) + max(0, -k + p), k][: N - abs(k - p)]
-                             for k in range(2 * p + 1)], [k - p for k in range(2 * p + 1)], shape=(N, N)))
+    M1 = [_band_csr(O, mm, d, 0) for d in range(3)]
     A = sps.kron(M1[2], sps.kron(M1[1], M1[0])).tocsr()
     A.sort_indices()
     rp, cols, vals = A.indptr.astype(np.int64), A.indices.astype(np.int64), A.data
@@ -120,10 +149,23 @@ def cpu_baseline(p, n_cells, threads):
     t0 = time.perf_counter()
     _, its = O.cg(rp, cols, vals, r, precond=1, max_it=1000, abs_tol=1e-20, rel_tol=1e-14)
     dt_m = time.perf_counter() - t0
+    # C5 sample: identity-preconditioned CG iterations (the reference's hot loop) on a 1024^2 GDM system
+    n5, it5 = 1024, 40
+    m5 = O.Mesh(2, 3, n5 - 1, -1.21, 1.21)
+    Mx, Lx = _band_csr(O, m5, 0, 0), _band_csr(O, m5, 0, 2)
+    A5 = (sps.kron(Lx, Mx) + sps.kron(Mx, Lx)).tocsr()
+    A5.sort_indices()
+    rp5, c5, v5 = A5.indptr.astype(np.int64), A5.indices.astype(np.int64), A5.data
+    b5 = np.ones(n5 * n5)
+    t0 = time.perf_counter()
+    _, its5 = O.cg(rp5, c5, v5, b5, precond=0, max_it=it5, abs_tol=0.0, rel_tol=0.0)
+    its5 = it5 if its5 < 0 else its5  # gdmo_cg returns -1 when max_it ends the solve (tolerance 0 here)
+    dt5 = (time.perf_counter() - t0) / its5
     return {
         "value": m.n_dofs / dt_n,
         "unit": "DoF-updates/s",
         "cores": threads,
+        "cores_visible": os.cpu_count(),
         "kind": "port",
         "cpu": _cpu_model(),
         "sample": "3D p=%d advection compute_rhs, reference per-cell algorithm (oracle/gdm_oracle.c), %d^3 cells = "
@@ -134,6 +176,13 @@ def cpu_baseline(p, n_cells, threads):
         "mass_solve": {"value": mm.n_dofs / dt_m, "unit": "DoF/s (one M^-1 r)", "cores": 1, "cg_iterations": int(its),
                        "sample": "24^3 cells p=%d: CSR mass (%d nnz) + SolverCG/Jacobi rel 1e-14, 1 thread"
                                  % (p, len(vals))},
+        "c4_wave": {"value": mw.n_dofs / dt_w, "unit": "DoF-updates/s (wave compute_rhs)", "cores": threads,
+                    "sample": "3D p=7 wave stiffness cell loop (wave/stiffness.h:151-181), %d^3 cells, %d z-slabs, "
+                              "%d application(s)" % (nw, threads, reps_w)},
+        "c5_cg": {"value": (n5 * n5) / dt5, "unit": "row-updates/s (one CG iteration = SpMV + 2 dots + 3 axpys)",
+                  "ms_per_iteration": dt5 * 1e3, "cores": 1,
+                  "sample": "2D p=3 %d^2 DoFs, CSR %d nnz (full (2p+1)^2 GDM sparsity), SolverCG + "
+                            "PreconditionIdentity, %d iterations, 1 thread" % (n5, len(v5), its5)},
     }
 
 
@@ -271,7 +320,7 @@ def main():
 
     achieved = BYTES_PER_DOF * lay["n_owned"] / (kern_ms * 1e-3) / 1e9
     mass = stage_ms = None
-    if world == 1:
+    if world == 1 and not args.metric_only:
         # the exact mass inverse (gdm_mass_solve; HIP events on the op stream) and one device-resident RK4
         # stage of the advection problem (AdvectionProblem.step / 4)
         op.time_op(2, dst, src[:lay["n_owned"]], None, 2)  # warm-up (first launches of the line-solve kernels)
@@ -296,11 +345,12 @@ def main():
             stage_ms = e0.elapsed_time(e1) / 12.0
             del prob
     traffic = None
-    if world == 1 and str(args.pmc) == "1":
+    if world == 1 and str(args.pmc) == "1" and not args.metric_only:
         traffic = pmc_traffic(args)
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and not args.metric_only:
         try:
+            # the box allots 16 host CPUs per GPU (os.cpu_count() shows the whole machine there)
             cpu = cpu_baseline(p, args.cpu_cells, args.cpu_threads or min(16, os.cpu_count() or 1))
         except Exception as e:  # the baseline never blocks the GPU line
             cpu = {"value": None, "error": str(e)}

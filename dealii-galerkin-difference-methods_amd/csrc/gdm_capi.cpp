@@ -1031,7 +1031,13 @@ void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
                   const char *what) {
     const LineTables &t = tab[ax];
     const bool aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(x_owned)) & 15) == 0;
-    if (v3 && t.l3 && (dir_kind == 1 || (len % 2 == 0 && aligned)))
+    // the v3 strided kernel addresses a wave's 64 lines through one buffer
+    // resource (num_records 0x7fffffff) with 32-bit position offsets: the
+    // line span (len - 1) * stride plus the 64 lanes must stay below 2^31
+    // bytes (3D meshes up to 645 vertices per direction), else the v2 kernel
+    // (64-bit addresses) runs
+    const bool span_ok = dir_kind != 1 || ((len - 1) * stride + 64) * 8 < (int64_t)0x7fffffff;
+    if (v3 && t.l3 && span_ok && (dir_kind == 1 || (len % 2 == 0 && aligned)))
       hip_check(gdmk_launch_mass3(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, t.l3, t.u3, t.d3,
                                   t.cst.data(), notab ? 0 : t.row_lo, notab ? (1 << 29) : t.row_hi, op->stream),
                 what);

@@ -463,8 +463,8 @@ int create_impl(int device, int64_t n_rows, int64_t n_cols, int64_t nnz, const i
     }
     // row blocks for the row-block kernel: consecutive rows with at most
     // CSR_NZB entries and CSR_BLOCK rows per block (a longer row alone)
+    std::vector<int64_t> hrp, rb;  // host staging: alive until the stream sync below
     if (n_rows > 0) {
-      std::vector<int64_t> hrp;
       const int64_t *r = rp;
       if (src_is_device) {
         hrp.resize((size_t)n_rows + 1);
@@ -473,18 +473,13 @@ int create_impl(int device, int64_t n_rows, int64_t n_cols, int64_t nnz, const i
         hip_check(hipStreamSynchronize(A->stream), "sync");
         r = hrp.data();
       }
-      std::vector<int64_t> rb;
-      int64_t row = 0, mx = 0, mn = INT64_MAX;
+      int64_t row = 0;
       rb.push_back(0);
       while (row < n_rows) {
         int64_t e = row + 1;
         while (e < n_rows && e - row < CSR_BLOCK && r[e + 1] - r[row] <= CSR_NZB) ++e;
         rb.push_back(e);
         row = e;
-      }
-      for (int64_t i = 0; i < n_rows; ++i) {
-        mx = std::max(mx, r[i + 1] - r[i]);
-        mn = std::min(mn, r[i + 1] - r[i]);
       }
       A->n_blocks = (int64_t)rb.size() - 1;
       hip_check(hipMalloc(&A->rb, sizeof(int64_t) * rb.size()), "hipMalloc row blocks");
@@ -493,11 +488,8 @@ int create_impl(int device, int64_t n_rows, int64_t n_cols, int64_t nnz, const i
       // the row-block kernel everywhere (measured on config 5: cut matrix with
       // rows of 49 and 1 entries 3.11 -> 1.62 ms, full 49-entry stencil
       // 3.97 -> 2.75 ms per SpMV); GDM_CSR_MODE=0: K lanes per row
-      (void)mx;
-      (void)mn;
       A->mode = 1;
       if (const char *env = std::getenv("GDM_CSR_MODE")) A->mode = std::atoi(env) == 1 ? 1 : 0;
-      hip_check(hipStreamSynchronize(A->stream), "sync");
     }
     hip_check(hipStreamSynchronize(A->stream), "sync");
   } catch (...) {
@@ -537,50 +529,6 @@ double read_scalar(gdm_csr *A, int slot) {
   hip_check(hipStreamSynchronize(A->stream), "sync");
   return A->S_host[0];
 }
-
-// GDM_CG_TRACE=1: after every CG iteration download the device state and check
-// the recurrence invariants on the host (debugging aid; prints to stderr)
-struct CgTrace {
-  bool on = false;
-  std::vector<int64_t> rp;
-  std::vector<uint32_t> ci;
-  std::vector<double> v, r, p, q, x, S;
-  void init(gdm_csr *A) {
-    on = std::getenv("GDM_CG_TRACE") != nullptr;
-    if (!on) return;
-    rp.resize(A->n_rows + 1);
-    ci.resize(std::max<int64_t>(A->nnz, 1));
-    v.resize(std::max<int64_t>(A->nnz, 1));
-    hip_check(hipStreamSynchronize(A->stream), "sync");
-    hip_check(hipMemcpy(rp.data(), A->rp, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost), "d2h");
-    hip_check(hipMemcpy(ci.data(), A->ci, sizeof(uint32_t) * ci.size(), hipMemcpyDeviceToHost), "d2h");
-    hip_check(hipMemcpy(v.data(), A->v, sizeof(double) * v.size(), hipMemcpyDeviceToHost), "d2h");
-  }
-  void step(gdm_csr *A, const double *xd, int it) {
-    if (!on) return;
-    const int64_t n = A->n_rows;
-    r.resize(n); p.resize(n); q.resize(n); x.resize(n); S.resize(S_N);
-    hip_check(hipStreamSynchronize(A->stream), "sync");
-    hip_check(hipMemcpy(r.data(), A->r, sizeof(double) * n, hipMemcpyDeviceToHost), "d2h");
-    hip_check(hipMemcpy(p.data(), A->p, sizeof(double) * n, hipMemcpyDeviceToHost), "d2h");
-    hip_check(hipMemcpy(q.data(), A->q, sizeof(double) * n, hipMemcpyDeviceToHost), "d2h");
-    hip_check(hipMemcpy(x.data(), xd, sizeof(double) * n, hipMemcpyDeviceToHost), "d2h");
-    hip_check(hipMemcpy(S.data(), A->S, sizeof(double) * S_N, hipMemcpyDeviceToHost), "d2h");
-    double rr = 0, pap = 0, dq = 0, nq = 0;
-    for (int64_t i = 0; i < n; ++i) {
-      double s = 0;
-      for (int64_t k = rp[i]; k < rp[i + 1]; ++k) s += v[k] * p[ci[k]];
-      dq = std::max(dq, std::fabs(s - q[i]));
-      nq = std::max(nq, std::fabs(s));
-      rr += r[i] * r[i];
-      pap += p[i] * s;
-    }
-    std::fprintf(stderr,
-                 "[cg-trace] it %d  S: rr %.6e gh %.6e gh_old %.6e pap %.6e | host rr %.6e pap %.6e |Ap-q| %.3e "
-                 "of %.3e\n",
-                 it, S[S_RR], S[S_GH + (it & 1)], S[S_GH + ((it - 1) & 1)], S[S_PAP], rr, pap, dq, nq);
-  }
-};
 
 }  // namespace
 
@@ -667,8 +615,6 @@ int gdm_csr_cg(gdm_csr *A, const double *b, double *x, int precond, int max_it, 
     res = std::sqrt(read_scalar(A, S_RR));
     const double tol = std::max(abs_tol, rel_tol * res);
     bool converged = res <= tol;
-    CgTrace trace;
-    trace.init(A);
     // p.Ap and r.r / r.z from grid-stride kernels over gs <= CG_GRID blocks
     // (the per-row-block SpMV partials and one partial per 256 rows made the
     // single-block reductions 100 us each at config 5)
@@ -683,7 +629,6 @@ int gdm_csr_cg(gdm_csr *A, const double *b, double *x, int precond, int max_it, 
       cg_update_kernel<<<gs, CSR_BLOCK, 0, A->stream>>>(n, x, A->r, A->p, A->q, dinv, A->S, its, A->part, gs);
       cg_reduce_kernel<<<1, RED_BLOCK, 0, A->stream>>>(A->part, gs, 2, S_RR, S_GH + (its & 1), A->S);
       hip_check(hipGetLastError(), "cg iteration");
-      if (its <= 40) trace.step(A, x, its);
       res = std::sqrt(read_scalar(A, S_RR));
       converged = res <= tol;
     }

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 namespace gdmk {
 
 // Fused Kronecker stencil: out = B_x M_y M_z + M_x B_y M_z + M_x M_y B_z (or
@@ -76,6 +78,20 @@ struct FaceArgs {
 };
 
 constexpr int FACE_CHUNK = 256;  // t0 nodes per workgroup of the face row kernel
+
+// hipFuncAttributeMaxDynamicSharedMemorySize is a per-device property of a
+// kernel: `mask` holds one bit per device that has it (a second thread racing
+// on the same device sets the same value again, which is harmless)
+inline hipError_t gdmk_set_lds_attr(const void *kernel, size_t lds, std::atomic<uint64_t> &mask) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const uint64_t bit = 1ull << (dev & 63);
+  if (mask.load(std::memory_order_acquire) & bit) return hipSuccess;
+  e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) mask.fetch_or(bit, std::memory_order_acq_rel);
+  return e;
+}
 
 }  // namespace gdmk
 

@@ -1482,12 +1482,11 @@ static hipError_t launch7_t(const StencilArgs &a, hipStream_t st) {
   using G = Geom7<P, R, NC, NP, BK>;
   static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget");
   const size_t lds = G::lds_bytes();
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)stencil7_kernel<P, R, NC, NP, BK, CH>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  {
+    // the LDS attribute is per device; one bit per device, set from any thread
+    static std::atomic<uint64_t> attr_mask{0};
+    hipError_t e = gdmk_set_lds_attr((const void *)stencil7_kernel<P, R, NC, NP, BK, CH>, lds, attr_mask);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   dim3 grid((a.Nx + G::TX - 1) / G::TX, (a.out_y1 - a.out_y0 + G::TY - 1) / G::TY,
             (a.out_z1 - a.out_z0 + a.zchunk - 1) / a.zchunk);
@@ -1513,12 +1512,11 @@ static hipError_t launch8_t(const StencilArgs &a, hipStream_t st) {
   using G = Geom8<P, R, NC, NP, BK>;
   static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget");
   const size_t lds = G::lds_bytes();
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)stencil8_kernel<P, R, NC, NP, BK, CH, PF, ZI>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  {
+    // the LDS attribute is per device; one bit per device, set from any thread
+    static std::atomic<uint64_t> attr_mask{0};
+    hipError_t e = gdmk_set_lds_attr((const void *)stencil8_kernel<P, R, NC, NP, BK, CH, PF, ZI>, lds, attr_mask);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   int nz = 0;
   for (int r = 0; r < 2; ++r)

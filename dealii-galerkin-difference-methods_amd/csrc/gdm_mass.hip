@@ -492,9 +492,10 @@ struct Ring3 {
 // (consecutive lanes = consecutive addresses: every load / store instruction
 // moves one contiguous 512-B row segment).  The loads stream Q positions ahead
 // of the forward recurrence through a register FIFO, across chunk borders.
-// Requires (len - 1) * stride + 64 entries to span < 2^31 bytes... (host-checked:
-// the offsets are 64-bit SGPR values, the lane offset is 32-bit).  src may
-// equal dst.
+// Requires ((len - 1) * stride + 64) * 8 < 2^31 bytes: the buffer resource's
+// num_records is 0x7fffffff and the position offsets are 32-bit (checked by
+// mass_solve_passes in gdm_capi.cpp, which runs the 64-bit-addressed v2
+// kernel for larger spans).  src may equal dst.
 template <int P>
 __global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel(const double *src, double *dst, int len, int64_t stride,
                                                            int64_t n_lines, int64_t A, int64_t B,
@@ -739,14 +740,9 @@ hipError_t launch_mass3_p(int dir_kind, const double *src, double *dst, int len,
   k.row_hi = row_hi;
   const unsigned grid = (unsigned)((n_lines + 63) / 64);
   if (dir_kind == 0) {
-    const size_t lds = Geo3<P>::lds_bytes();
-    static bool attr = false;
-    if (!attr) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mass3_rows_kernel<P>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-      attr = true;
-    }
+    // <= 59 KB (p = 7): within the 64 KB default, no attribute needed
+    constexpr size_t lds = Geo3<P>::lds_bytes();
+    static_assert(lds <= 64 * 1024, "mass3_rows_kernel LDS above the default limit");
     hipLaunchKernelGGL(mass3_rows_kernel<P>, dim3(grid), dim3(64), lds, st, src, dst, len, n_lines, lrow, urow, invd, k);
   } else {
     hipLaunchKernelGGL(mass3_strided_kernel<P>, dim3(grid), dim3(64), 0, st, src, dst, len, stride, n_lines, A, B,

@@ -40,8 +40,8 @@ hipError_t gdmk_launch_rk_update(int64_t n, double beta, const double *k, const 
 // distribute v[last] = v[first], mode 1 condense v[first] += v[last], v[last] = 0
 hipError_t gdmk_launch_periodic(double *v, const int64_t N[3], int d, int mode, hipStream_t st);
 // distributed mass inverse, interface correction (gdm_mass_solve_interface):
-// per line i of the plane, b = S_lo [ghost below (p planes); owned top p],
-// t = S_hi [owned bottom p; ghost above (p planes)], then for owned planes k in
+// per line i of the plane, b = S_lo [ghost below (p planes); owned bottom p],
+// t = S_hi [owned top p; ghost above (p planes)], then for owned planes k in
 // [k_begin, k_end): x_k -= VW[k][0:p] . t + VW[k][p:2p] . b
 hipError_t gdmk_launch_spike(int p, double *x_local, int64_t plane_size, int64_t own_off, int n_planes, int has_lo,
                              int has_hi, const double *VW, const double *S, int k_begin, int k_end, hipStream_t st);

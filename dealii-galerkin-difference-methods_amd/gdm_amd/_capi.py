@@ -5,6 +5,7 @@ There is no CPU fallback -- if the library or a GPU is missing, operator
 construction raises GdmError.
 """
 import ctypes
+import importlib.util
 import os
 import re
 
@@ -80,6 +81,24 @@ class Layout(ctypes.Structure):
 _lib = None
 
 
+def torch_hip_runtime():
+    """Path of the HIP runtime torch ships (None when torch is absent).
+
+    libgdm_hip.so NEEDs `libamdhip64.so.7` (RUNPATH /opt/rocm/lib) while
+    libtorch_hip NEEDs torch's own copy, whose soname is the same
+    `libamdhip64.so.7`.  Loaded first, the engine would map /opt/rocm's
+    runtime and a later `import torch` a second one (plus a second
+    libhsa-runtime64): two HIP runtimes in one process.  Preloading torch's
+    copy makes the dynamic linker satisfy the engine's NEEDED entry by soname
+    and torch's by file identity, so every Python process maps exactly one.
+    """
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return None
+    path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    return path if os.path.exists(path) else None
+
+
 def load():
     """Load libgdm_hip.so (fails loudly when it has not been built)."""
     global _lib
@@ -87,6 +106,9 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise GdmError("libgdm_hip.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+    rt = torch_hip_runtime()
+    if rt is not None:
+        ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
     L = ctypes.CDLL(LIB_PATH)
     P, i32, i64, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
     sig = {

@@ -291,6 +291,31 @@ def test_full_size_properties_3d_p5():
     assert float(err) < 1e-12
 
 
+@pytest.mark.gpu
+def test_mass_solve_line_span_above_2gb():
+    """A z-line spanning more than 2^31 bytes ((Z-1) * X * Y * 8 = 2.29e9 at
+    640 x 640 x 700 vertices, 2.3 GB per vector): the v3 strided kernel's
+    32-bit buffer offsets cannot reach it, so the pass must take the 64-bit
+    addressed v2 kernel.  M^-1 (M u) == u over the whole vector,
+    and over the last z-planes (the part a 32-bit offset would drop)."""
+    g = _gdm()
+    n = (639, 639, 699)
+    op = g.GdmOperator(3, 5, n, 0.0, 1.0, "mass")
+    N = op.n_owned
+    assert (n[2]) * 640 * 640 * 8 > 2 ** 31
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    u = torch.rand(N, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+    Mu = op.new_vector(local=False)
+    op.mass_apply(u, Mu)
+    x = op.new_vector(local=False)
+    op.mass_solve(Mu, x)
+    del Mu
+    err = torch.linalg.norm(x - u) / torch.linalg.norm(u)
+    tail = slice(N - 40 * 640 * 640, N)
+    err_tail = torch.linalg.norm(x[tail] - u[tail]) / torch.linalg.norm(u[tail])
+    assert float(err) < 1e-12 and float(err_tail) < 1e-12, (float(err), float(err_tail))
+
+
 @pytest.mark.parametrize("n_ranks,shape,p,kind", [
     (2, (20, 18, 31), 5, "advection"),
     (3, (140, 70, 100), 5, "advection"),
