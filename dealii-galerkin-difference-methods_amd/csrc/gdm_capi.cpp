@@ -97,6 +97,8 @@ struct LineTables {
 struct SpikeTables {
   bool built = false;
   double eps = 0.0;        // largest dropped far-spike entry over all slabs
+  int rounds = 0;          // refinement exchanges (-1: partition refused)
+  double *G0 = nullptr;    // device [2p][plane]: saved slab-solve edge planes (rounds > 0)
   int n_planes = 0;        // owned planes of this rank
   int has_lo = 0, has_hi = 0;
   LineTables slab;         // A_r
@@ -922,12 +924,16 @@ std::vector<double> interface_rows(const std::vector<double> &Vb, const std::vec
 }
 
 // Largest entry of the couplings the truncated interface systems drop: the
-// far spikes W_s^bot (slab s's last p rows of W) and V_s^top over all slabs.
-double spike_eps(const gdm::Band &M, int p, unsigned n_cells, unsigned n_ranks) {
+// far spikes W_s^bot (slab s's last p rows of W) and V_s^top over all slabs;
+// min_planes = the thinnest slab.
+double spike_eps(const gdm::Band &M, int p, unsigned n_cells, unsigned n_ranks, int *min_planes = nullptr) {
   double eps = 0.0;
+  int mn = 1 << 30;
   for (unsigned s = 0; s < n_ranks; ++s) {
     const gdm::Slab sl = gdm::slab_partition(n_cells, n_ranks, s);
     const int pb = (int)sl.plane_begin, pe = (int)std::max(sl.plane_begin, sl.plane_end), n = pe - pb;
+    mn = std::min(mn, n);
+    if (min_planes) *min_planes = mn;
     if (n_ranks == 1) return 0.0;
     if (n < p) return 1.0;  // a slab thinner than the interface
     const SlabSpikes sp = slab_spikes(M, p, pb, pe);
@@ -940,14 +946,35 @@ double spike_eps(const gdm::Band &M, int p, unsigned n_cells, unsigned n_ranks) 
   return eps;
 }
 
+// Refinement rounds of the truncated interface systems.  The 2p x 2p system
+// of interface (r, r+1) drops the couplings W_r^bot x_{r-1}^bot and
+// V_{r+1}^top x_{r+2}^top (entries <= eps).  A round evaluates them at the
+// current interface values, moves them to the right-hand sides (one more
+// p-plane exchange) and re-solves: block Jacobi on the reduced SPIKE system,
+// error ~ eps^(m+1) after m rounds (C4 at 8 ranks: eps = 2e-8, one round,
+// 4e-16).  Rounds need the first and last p planes of every slab distinct.
+constexpr int kSpikeMaxRounds = 3;
+int spike_rounds(double eps, int min_planes, int p) {
+  if (eps <= kSpikeTol) return 0;
+  if (eps >= 1e-2 || min_planes < 2 * p) return -1;
+  double e = eps;
+  for (int m = 1; m <= kSpikeMaxRounds; ++m) {
+    e *= eps;
+    if (e <= kSpikeTol) return m;
+  }
+  return -1;
+}
+
 void build_spike(gdm_op *op) {
   SpikeTables &T = op->spike;
   const int p = op->p, q = op->dim - 1;
   const unsigned nc = (unsigned)op->mesh.n_subdivisions[q], R = (unsigned)op->mesh.n_ranks, r = (unsigned)op->mesh.rank;
   const gdm::Band M = gdm::assemble_1d(p, nc, (op->mesh.hi[q] - op->mesh.lo[q]) / nc).M;
   T.built = true;
-  T.eps = spike_eps(M, p, nc, R);
-  if (T.eps > kSpikeTol) return;
+  int min_planes = 0;
+  T.eps = spike_eps(M, p, nc, R, &min_planes);
+  T.rounds = spike_rounds(T.eps, min_planes, p);
+  if (T.rounds < 0) return;
   auto planes = [&](unsigned s) {
     const gdm::Slab sl = gdm::slab_partition(nc, R, s);
     return std::make_pair((int)sl.plane_begin, (int)std::max(sl.plane_begin, sl.plane_end));
@@ -996,6 +1023,8 @@ void build_spike(gdm_op *op) {
   }
   T.VW = keep(op, dev_upload(VW));
   T.S = keep(op, dev_upload(S));
+  if (T.rounds > 0)
+    T.G0 = keep(op, dev_upload(std::vector<double>((size_t)2 * p * std::max<int64_t>(L.plane_size, 1), 0.0)));
 }
 
 // the line solves of M^-1 along every kernel axis; `part` replaces the
@@ -1408,6 +1437,21 @@ int gdm_mass_spike_eps(const gdm_mesh_desc *mesh, double *eps_host) {
   GDM_GUARD_END
 }
 
+int gdm_mass_spike_rounds(const gdm_mesh_desc *mesh, int *rounds) {
+  if (!mesh || !rounds) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  if (mesh->dim < 1 || mesh->dim > 3 || mesh->fe_degree < 1 || mesh->n_ranks < 1)
+    return fail(GDM_ERR_ARG, "bad mesh description");
+  const int q = mesh->dim - 1;
+  const unsigned nc = (unsigned)mesh->n_subdivisions[q];
+  const gdm::Band M = gdm::assemble_1d(mesh->fe_degree, nc, (mesh->hi[q] - mesh->lo[q]) / nc).M;
+  int min_planes = 0;
+  const double eps = spike_eps(M, mesh->fe_degree, nc, (unsigned)mesh->n_ranks, &min_planes);
+  *rounds = spike_rounds(eps, min_planes, mesh->fe_degree);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
 int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   if (op->mesh.periodic) return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_slab: periodic mesh");
@@ -1419,12 +1463,13 @@ int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned) {
     return GDM_OK;
   }
   if (!op->spike.built) build_spike(op);
-  if (op->spike.eps > kSpikeTol) {
+  if (op->spike.rounds < 0) {
     char msg[256];
     std::snprintf(msg, sizeof msg,
-                  "gdm_mass_solve_slab: slabs too thin for the truncated interface system (dropped coupling %.3g > "
-                  "%.1g); use gdm_mass_solve_cg or fewer ranks",
-                  op->spike.eps, kSpikeTol);
+                  "gdm_mass_solve_slab: slabs too thin for the interface systems (dropped coupling %.3g, %d "
+                  "refinement rounds do not reach %.1g or a slab has < 2p planes); use gdm_mass_solve_cg or fewer "
+                  "ranks",
+                  op->spike.eps, kSpikeMaxRounds, kSpikeTol);
     return fail(GDM_ERR_UNSUPPORTED, msg);
   }
   mass_solve_passes(op, rhs_owned, x_owned, &op->spike.slab);
@@ -1435,17 +1480,36 @@ int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned) {
 int gdm_mass_solve_interface(gdm_op *op, double *x_local) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   if (op->mesh.n_ranks == 1) return GDM_OK;
-  if (!op->spike.built || op->spike.eps > kSpikeTol)
+  if (!op->spike.built || op->spike.rounds < 0)
     return fail(GDM_ERR_STATE, "gdm_mass_solve_interface: call gdm_mass_solve_slab first");
   if (op->layout.n_owned > 0 && !x_local) return fail(GDM_ERR_ARG, "NULL vector");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   const SpikeTables &S = op->spike;
-  if (S.k_end > S.k_begin && (S.has_lo || S.has_hi))
+  if ((S.k_end > S.k_begin || S.rounds > 0) && (S.has_lo || S.has_hi))
     hip_check(gdmk_launch_spike(op->p, x_local, op->layout.plane_size,
                                 (int64_t)op->layout.ghost_planes_below * op->layout.plane_size, S.n_planes, S.has_lo,
-                                S.has_hi, S.VW, S.S, S.k_begin, S.k_end, op->stream),
+                                S.has_hi, S.VW, S.S, S.k_begin, S.k_end, 0, 0, S.rounds > 0 ? S.G0 : nullptr,
+                                op->stream),
               "spike");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_mass_solve_interface_round(gdm_op *op, double *x_local, int round) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->mesh.n_ranks == 1) return fail(GDM_ERR_STATE, "gdm_mass_solve_interface_round: one rank needs no rounds");
+  if (!op->spike.built || op->spike.rounds < 0)
+    return fail(GDM_ERR_STATE, "gdm_mass_solve_interface_round: call gdm_mass_solve_slab first");
+  if (round < 0 || round >= op->spike.rounds) return fail(GDM_ERR_ARG, "round out of range [0, rounds)");
+  if (op->layout.n_owned > 0 && !x_local) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  const SpikeTables &S = op->spike;
+  hip_check(gdmk_launch_spike(op->p, x_local, op->layout.plane_size,
+                              (int64_t)op->layout.ghost_planes_below * op->layout.plane_size, S.n_planes, S.has_lo,
+                              S.has_hi, S.VW, S.S, S.k_begin, S.k_end, 1, round, S.G0, op->stream),
+            "spike round");
   return GDM_OK;
   GDM_GUARD_END
 }

@@ -876,7 +876,7 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
         const int g = t.wv + ps * NP;
         if (g < G::NG) {
           if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, tt, u[slot], g, V1);
-          write_ab8<P, R, NC, NP, BK>(tt, g, V1);
+          if (!GDM_DBG(a, 64)) write_ab8<P, R, NC, NP, BK>(tt, g, V1);
           if (t.ncw > 0) {
             XWall<P, BK> xw0;
             xwall8_calc<P, R, NC, NP, BK>(tt, u[slot], g, xpre, xw0);
@@ -1121,7 +1121,7 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
   // retire output plane zz - p
   constexpr int rslot = (JP - P + 2 * W) % W;
   const int zo = zz - P;
-  if (zo >= t.zc0 && zo < t.zc1) {
+  if (zo >= t.zc0 && zo < t.zc1 && !GDM_DBG(a, 32)) {
     const int Nx = a.Nx, x = t.x0 + t.lane;
     double *orow = a.dst + ((int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) + (ybase - a.out_y0)) * Nx + x;
     if (full) {

@@ -159,10 +159,19 @@ __global__ void __launch_bounds__(256) vmul_kernel(int64_t n, const double *__re
 // interface unknowns of both slab edges in registers, then a rank-2p update
 // of the line's planes.  The edge planes are read before any plane is written
 // (one thread owns its line), so the update is in place.
+//
+// mode 1 (refinement round, thin slabs): instead of the update, the slab's
+// edge planes g_first / g_last (saved to G0 [2p][ps] at round 0) are replaced
+// by the right-hand sides of the next interface systems with the dropped
+// far-spike couplings evaluated at the current interface values:
+//   first p planes: g_first - V[0:p] t,  last p planes: g_last - W[n-p:n] b;
+// the caller then exchanges ghost planes again.  mode 0 with G0 != NULL
+// restores the saved edge planes before the update.
 template <int P>
 __global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps, int64_t own_off, int n, int has_lo,
                                                     int has_hi, const double *__restrict__ VW,
-                                                    const double *__restrict__ S, int k_begin, int k_end) {
+                                                    const double *__restrict__ S, int k_begin, int k_end, int mode,
+                                                    int round, double *__restrict__ G0) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ps; i += (int64_t)gridDim.x * blockDim.x) {
     double *xo = x_local + own_off + i;
     double b[P], t[P], in[2 * P];
@@ -196,6 +205,35 @@ __global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps,
         t[j] = s;
       }
     }
+    if (mode == 1) {
+#pragma unroll
+      for (int a = 0; a < P; ++a) {
+        double gf = xo[(int64_t)a * ps], gl = xo[(int64_t)(n - P + a) * ps];
+        if (round == 0) {
+          G0[(int64_t)a * ps + i] = gf;
+          G0[(int64_t)(P + a) * ps + i] = gl;
+        } else {
+          gf = G0[(int64_t)a * ps + i];
+          gl = G0[(int64_t)(P + a) * ps + i];
+        }
+        const double *vf = VW + (size_t)a * 2 * P, *wl = VW + (size_t)(n - P + a) * 2 * P + P;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          gf = fma(-vf[j], t[j], gf);
+          gl = fma(-wl[j], b[j], gl);
+        }
+        xo[(int64_t)a * ps] = gf;
+        xo[(int64_t)(n - P + a) * ps] = gl;
+      }
+      continue;
+    }
+    if (G0) {
+#pragma unroll
+      for (int a = 0; a < P; ++a) {
+        xo[(int64_t)a * ps] = G0[(int64_t)a * ps + i];
+        xo[(int64_t)(n - P + a) * ps] = G0[(int64_t)(P + a) * ps + i];
+      }
+    }
     for (int k = k_begin; k < k_end; ++k) {
       const double *vw = VW + (size_t)k * 2 * P;
       double c = 0.0;
@@ -212,13 +250,13 @@ __global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps,
 
 extern "C" hipError_t gdmk_launch_spike(int p, double *x_local, int64_t ps, int64_t own_off, int n, int has_lo,
                                        int has_hi, const double *VW, const double *S, int k_begin, int k_end,
-                                       hipStream_t st) {
-  if (ps <= 0 || k_end <= k_begin) return hipSuccess;
+                                       int mode, int round, double *G0, hipStream_t st) {
+  if (ps <= 0 || (mode == 0 && !G0 && k_end <= k_begin)) return hipSuccess;
   const unsigned blocks = (unsigned)std::min<int64_t>((ps + 255) / 256, 4096);
 #define GDM_SPIKE(PP)                                                                                           \
   case PP:                                                                                                      \
     hipLaunchKernelGGL(gdmk::spike_kernel<PP>, dim3(blocks), dim3(256), 0, st, x_local, ps, own_off, n, has_lo, \
-                       has_hi, VW, S, k_begin, k_end);                                                          \
+                       has_hi, VW, S, k_begin, k_end, mode, round, G0);                                         \
     break;
   switch (p) {
     GDM_SPIKE(1)

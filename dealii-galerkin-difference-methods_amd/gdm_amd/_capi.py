@@ -140,6 +140,8 @@ def load():
         "gdm_mass_spike_eps": [P, P],
         "gdm_mass_solve_slab": [P, P, P],
         "gdm_mass_solve_interface": [P, P],
+        "gdm_mass_solve_interface_round": [P, P, i32],
+        "gdm_mass_spike_rounds": [P, ctypes.POINTER(ctypes.c_int)],
         "gdm_synchronize": [P],
         "gdm_malloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
         "gdm_free": [P, P],
@@ -210,6 +212,15 @@ def mesh_desc(dim, fe_degree, n_subdivisions, lo=0.0, hi=1.0, n_ranks=1, rank=0,
         m.hi[d] = float(hi) if d < dim else 1.0
     m.n_ranks, m.rank, m.periodic = n_ranks, rank, periodic
     return m
+
+
+def mass_spike_rounds(dim, fe_degree, n_subdivisions, n_ranks, lo=0.0, hi=1.0):
+    """Refinement rounds (extra p-plane exchanges) the distributed mass
+    inverse needs for this partition; -1: refused (pure host, no GPU)."""
+    r = ctypes.c_int(0)
+    m = mesh_desc(dim, fe_degree, n_subdivisions, lo, hi, n_ranks)
+    check(load().gdm_mass_spike_rounds(ctypes.byref(m), ctypes.byref(r)), "gdm_mass_spike_rounds")
+    return r.value
 
 
 def mass_spike_eps(dim, fe_degree, n_subdivisions, n_ranks, lo=0.0, hi=1.0):

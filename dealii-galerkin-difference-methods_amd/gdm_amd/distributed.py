@@ -208,25 +208,31 @@ class DistributedMassSolve:
 
 
 class SlabMassSolve:
-    """x = M^-1 r across slab ranks by the truncated SPIKE scheme of
+    """x = M^-1 r across slab ranks by the SPIKE scheme of
     gdm_mass_solve_slab / gdm_mass_solve_interface (include/gdm_hip.h): the
     slab-local solve, one ghost-plane exchange (the same p planes as the
-    stencil's update_ghost_values, advection/stiffness.h:343) and the
-    interface correction.  Moves 2 p planes per rank and solve, against the
-    whole vector twice for DistributedMassSolve's transposes.
+    stencil's update_ghost_values, advection/stiffness.h:343), `rounds`
+    refinement rounds of one more exchange each for slabs too thin for the
+    truncated interface systems (gdm_mass_spike_rounds; C4 at 8 ranks: one),
+    and the interface correction.  Moves 2 p planes per rank and exchange,
+    against the whole vector twice for DistributedMassSolve's transposes.
 
     `op` is the rank's GdmOperator (or any object with mass_solve_slab /
-    mass_solve_interface / owned_view), `halo` its HaloExchange (None on one
-    rank).  solve(rhs_owned, x_local) returns the owned view of x_local."""
+    mass_solve_interface[_round] / owned_view), `halo` its HaloExchange (None on
+    one rank).  solve(rhs_owned, x_local) returns the owned view of x_local."""
 
-    def __init__(self, op, halo):
-        self.op, self.halo = op, halo
+    def __init__(self, op, halo, rounds=0):
+        self.op, self.halo, self.rounds = op, halo, int(rounds)
 
     def solve(self, rhs_owned, x_local):
         x_owned = self.op.owned_view(x_local)
         self.op.mass_solve_slab(rhs_owned, x_owned)
         if self.halo is not None:
             self.halo.exchange(x_local)
+        for k in range(self.rounds):
+            self.op.mass_solve_interface_round(x_local, k)
+            if self.halo is not None:
+                self.halo.exchange(x_local)
         self.op.mass_solve_interface(x_local)
         return x_owned
 
@@ -236,13 +242,14 @@ SPIKE_TOL = 1e-15
 
 def make_mass_solver(op, halo, dim, p, n_subdivisions, n_ranks, rank, lo=0.0, hi=1.0, group=None):
     """The distributed exact mass inverse for this partition: SlabMassSolve
-    when the slabs are thick enough for the truncated interface systems
-    (gdm_mass_spike_eps <= 1e-15), else the transposes of
-    DistributedMassSolve.  Both expose solve(rhs_owned, x_local) -> owned."""
+    (with the refinement rounds gdm_mass_spike_rounds asks for), else -- a
+    slab thinner than 2p planes -- the transposes of DistributedMassSolve.
+    Both expose solve(rhs_owned, x_local) -> owned."""
     from . import _capi
 
-    if _capi.mass_spike_eps(dim, p, n_subdivisions, n_ranks, lo, hi) <= SPIKE_TOL:
-        return SlabMassSolve(op, halo)
+    rounds = _capi.mass_spike_rounds(dim, p, n_subdivisions, n_ranks, lo, hi)
+    if rounds >= 0:
+        return SlabMassSolve(op, halo, rounds)
     ns = list(n_subdivisions) if hasattr(n_subdivisions, "__len__") else [n_subdivisions] * dim
     ds = DistributedMassSolve(dim, [n + 1 for n in ns[:dim]], n_ranks, rank, op=op, group=group)
 

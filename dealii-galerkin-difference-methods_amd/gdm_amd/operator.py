@@ -199,6 +199,18 @@ class GdmOperator:
         check(self.lib.gdm_mass_solve_slab(self.h, _ptr(rhs_owned), _ptr(x_owned)), "gdm_mass_solve_slab")
         return x_owned
 
+    def mass_solve_interface_round(self, x_local, round_):
+        """Distributed exact mass inverse, refinement round `round_` of
+        gdm_mass_spike_rounds (thin slabs): the slab's edge planes become the
+        next interface systems' right-hand sides; exchange the ghost planes of
+        x_local again afterwards."""
+        if x_local.numel() != self.n_local:
+            raise GdmError("mass_solve_interface_round: x has %d entries, expected n_local %d"
+                           % (x_local.numel(), self.n_local))
+        check(self.lib.gdm_mass_solve_interface_round(self.h, _ptr(x_local), int(round_)),
+              "gdm_mass_solve_interface_round")
+        return x_local
+
     def mass_solve_interface(self, x_local):
         """Distributed exact mass inverse, step 2 (gdm_mass_solve_interface):
         the owned part of x_local (ghost planes = the neighbours' slab solves)

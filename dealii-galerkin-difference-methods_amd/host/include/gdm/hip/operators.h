@@ -390,20 +390,27 @@ class MassMatrixOperator {
     }
     return it;
   }
-  // Multi-rank exact solve (the truncated SPIKE scheme of
-  // gdm_mass_solve_slab / gdm_mass_solve_interface): slab-local solve, one
-  // ghost-plane exchange through `comm`, interface correction.  Usable when
-  // spike_available() (slabs thick enough for the dropped coupling to stay
-  // below 1e-15); x_owned may alias b_owned.
-  bool spike_available() const {
-    double eps = 1.0;
-    return gdm_mass_spike_eps(&discretization.get_mesh(), &eps) == GDM_OK && eps <= 1e-15;
+  // Multi-rank exact solve (the SPIKE scheme of gdm_mass_solve_slab /
+  // gdm_mass_solve_interface): slab-local solve, one ghost-plane exchange
+  // through `comm`, spike_rounds() refinement rounds of one more exchange
+  // each (slabs too thin for the truncated interface systems, e.g. C4 at 8
+  // ranks), interface correction.  Usable when spike_available() (every slab
+  // has >= 2p planes and the rounds reach 1e-15); x_owned may alias b_owned.
+  int spike_rounds() const {
+    int rounds = -1;
+    return gdm_mass_spike_rounds(&discretization.get_mesh(), &rounds) == GDM_OK ? rounds : -1;
   }
+  bool spike_available() const { return spike_rounds() >= 0; }
   void solve_spike(double *x_owned, const double *b_owned, Communicator &comm) const {
     if (sp_x.size() != (std::size_t)layout.n_local) sp_x.reinit(op, layout.n_local);
+    if (sp_rounds < 0) sp_rounds = spike_rounds();
     double *own = sp_x.get_values() + layout.ghost_planes_below * layout.plane_size;
     check(gdm_mass_solve_slab(op, b_owned, own), "gdm_mass_solve_slab");
     comm.update_ghost_values(op, sp_x);
+    for (int k = 0; k < sp_rounds; ++k) {
+      check(gdm_mass_solve_interface_round(op, sp_x.get_values(), k), "gdm_mass_solve_interface_round");
+      comm.update_ghost_values(op, sp_x);
+    }
     check(gdm_mass_solve_interface(op, sp_x.get_values()), "gdm_mass_solve_interface");
     check(gdm_memcpy_d2d(op, x_owned, own, sizeof(double) * layout.n_owned), "gdm_memcpy_d2d");
   }
@@ -415,6 +422,7 @@ class MassMatrixOperator {
   gdm_layout layout{};
   mutable DeviceVector cg_p, cg_r, cg_z, cg_Ap, cg_invdiag;  // solve_distributed work vectors
   mutable DeviceVector sp_x;                                  // solve_spike local vector
+  mutable int sp_rounds = -1;                                 // solve_spike refinement rounds (cached)
 };
 
 // deal.II DiscreteTime: fixed steps, the last one shrunk to hit end_t or, when

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 6
+#define GDM_HIP_ABI_VERSION 7
 
 enum gdm_status {
   GDM_OK = 0,
@@ -195,14 +195,24 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned);
  * boundary (the same for every line) corrects the slab:
  *   gdm_mass_solve_slab(op, rhs_owned, x_owned)   x = (A_r^-1 (x) M_y^-1 (x) M_x^-1) rhs
  *   <copy x_owned into the owned part of a local vector; ghost exchange>
+ *   for round in [0, rounds):                        (thin slabs only)
+ *     gdm_mass_solve_interface_round(op, x_local, round); <ghost exchange>
  *   gdm_mass_solve_interface(op, x_local)          owned part of x_local = M^-1 rhs
- * Exact up to the dropped coupling of the far spikes, which decays
- * geometrically with the slab thickness: gdm_mass_spike_eps (pure host)
- * reports it; the solve refuses (GDM_ERR_UNSUPPORTED) when it exceeds 1e-15
- * (e.g. slabs thinner than ~48 planes at p = 5).  n_ranks == 1: the slab solve
- * is gdm_mass_solve and the interface call a no-op. */
+ * The truncated interface systems drop the far-spike couplings (entries
+ * <= gdm_mass_spike_eps, pure host; decays geometrically with the slab
+ * thickness).  When that exceeds 1e-15 (slabs thinner than ~48 planes at p = 5,
+ * e.g. C4 at 8 ranks: 32 planes, p = 7, eps 2e-8) gdm_mass_spike_rounds
+ * (pure host) returns the number m of refinement rounds: each evaluates the
+ * dropped couplings at the current interface values, moves them into the
+ * slab's edge planes (the right-hand sides of the next interface systems) and
+ * needs one more ghost exchange of the same p planes; the error after m rounds
+ * is ~eps^(m+1).  rounds = -1: refused (GDM_ERR_UNSUPPORTED from the slab
+ * solve; a slab with fewer than 2p planes or eps too large).  n_ranks == 1:
+ * the slab solve is gdm_mass_solve and the interface call a no-op. */
 int gdm_mass_spike_eps(const gdm_mesh_desc *mesh, double *eps_host);
+int gdm_mass_spike_rounds(const gdm_mesh_desc *mesh, int *rounds);
 int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned);
+int gdm_mass_solve_interface_round(gdm_op *op, double *x_local, int round);
 int gdm_mass_solve_interface(gdm_op *op, double *x_local);
 
 /* x_owned = M^-1 rhs_owned by SolverCG on the matrix-free mass operator with

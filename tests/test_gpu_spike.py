@@ -6,7 +6,10 @@ neighbours' edge planes (what HaloExchange / MPI do between processes).
 Reference: the one-rank exact Kronecker inverse gdm_mass_solve, itself pinned
 to CG(1e-14) on the oracle's assembled mass matrix (test_gpu_parity.py) --
 the reference's *Problem::solve (advection/problem.h:236-267).
-Tolerance: rel-L2 <= 1e-13 (the truncated interface coupling is < 1e-15)."""
+Thin slabs (C4 at 8 ranks: 32 planes at p = 7, far-spike coupling 2e-8) run
+the refinement rounds of gdm_mass_spike_rounds (gdm_mass_solve_interface_round
++ one more exchange each).
+Tolerance: rel-L2 <= 1e-13 (the remaining interface coupling is < 1e-15)."""
 import numpy as np
 import pytest
 
@@ -37,10 +40,15 @@ def _exchange(ops, xs):
 
 @pytest.mark.parametrize("dim,p,n,R", [(3, 5, (12, 10, 130), 2), (3, 5, (9, 8, 200), 3), (2, 3, (20, 150), 3),
                                        (1, 5, 400, 4), (3, 7, (8, 9, 240), 2), (2, 9, (12, 260), 2),
-                                       (3, 1, (6, 5, 120), 4)])
+                                       (3, 1, (6, 5, 120), 4), (3, 7, (8, 9, 255), 8), (2, 5, (30, 150), 6),
+                                       (3, 7, (255, 255, 255), 8)])
 def test_slab_mass_solve_matches_single_rank(dim, p, n, R):
     import gdm_amd
 
+    rounds = gdm_amd._capi.mass_spike_rounds(dim, p, n, R)
+    assert rounds >= 0
+    if (p, R) == (7, 8):  # the C4 partition: one refinement round
+        assert rounds == 1
     one = gdm_amd.GdmOperator(dim, p, n, 0.0, 1.0, "mass")
     N = one.n_owned
     r = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, N)).cuda()
@@ -56,19 +64,24 @@ def test_slab_mass_solve_matches_single_rank(dim, p, n, R):
         xs.append(x)
     torch.cuda.synchronize()
     _exchange(ops, xs)
+    for k in range(rounds):
+        for op, x in zip(ops, xs):
+            op.mass_solve_interface_round(x, k)
+        torch.cuda.synchronize()
+        _exchange(ops, xs)
     for op, x in zip(ops, xs):
         op.mass_solve_interface(x)
     got = torch.cat([op.owned_view(x) for op, x in zip(ops, xs)])
     assert float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)) < 1e-13
 
 
-def test_slab_mass_solve_refuses_thin_slabs():
-    """C4 on 8 ranks (32 planes at p = 7): the dropped coupling exceeds 1e-15,
-    the slab solve refuses instead of returning an approximate inverse."""
+def test_slab_mass_solve_refuses_slabs_thinner_than_2p():
+    """8 ranks of p = 7 on 100 cells (12-13 planes < 2p): refused instead of
+    an approximate inverse."""
     import gdm_amd
 
-    assert gdm_amd._capi.mass_spike_eps(3, 7, 255, 8) > 1e-15
-    op = gdm_amd.GdmOperator(3, 7, (8, 8, 255), 0.0, 1.0, "mass", n_ranks=8, rank=3)
+    assert gdm_amd._capi.mass_spike_rounds(3, 7, (8, 8, 100), 8) == -1
+    op = gdm_amd.GdmOperator(3, 7, (8, 8, 100), 0.0, 1.0, "mass", n_ranks=8, rank=3)
     x = op.new_vector(False)
     with pytest.raises(gdm_amd.GdmError, match="too thin"):
         op.mass_solve_slab(x, x)

@@ -334,7 +334,7 @@ class _NpSpikeOp:
         x.numpy()[:] = v.reshape(-1)
         return x
 
-    def mass_solve_interface(self, x_local):
+    def _interface(self, x_local):
         p, P, r = self.p, self.plane, self.rank
         gb = self.L["ghost_planes_below"]
         a = x_local.numpy().reshape(-1, P)
@@ -351,6 +351,25 @@ class _NpSpikeOp:
             _, _, Wh = self._spikes(r + 1)
             S = np.block([[np.eye(p), V[-p:]], [Wh[:p], np.eye(p)]])
             t = np.linalg.solve(S, np.concatenate([own[-p:], a[gb + n:gb + n + p]]))[p:]
+        return own, V, W, b, t
+
+    def mass_solve_interface_round(self, x_local, k):
+        """refinement round: the edge planes become g - (dropped far-spike
+        couplings at the current interface values)"""
+        p = self.p
+        own, V, W, b, t = self._interface(x_local)
+        if k == 0:
+            self.G0 = (own[:p].copy(), own[-p:].copy())
+        own[:p] = self.G0[0] - V[:p] @ t
+        own[-p:] = self.G0[1] - W[-p:] @ b
+        return x_local
+
+    def mass_solve_interface(self, x_local):
+        p = self.p
+        own, V, W, b, t = self._interface(x_local)
+        if getattr(self, "G0", None) is not None:
+            own[:p], own[-p:] = self.G0
+            self.G0 = None
         own -= V @ t + W @ b
         return x_local
 
@@ -371,24 +390,29 @@ def _spike_worker(rank, world, port, dim, p, n, q):
         L = op.L
         mine = torch.from_numpy(r[L["owned_plane_begin"] * op.plane:L["owned_plane_end"] * op.plane].copy())
         x_local = torch.zeros(L["n_local"], dtype=torch.float64)
-        x = SlabMassSolve(op, halo).solve(mine, x_local)
+        rounds = _capi.mass_spike_rounds(dim, p, list(n), world)
+        x = SlabMassSolve(op, halo, rounds).solve(mine, x_local)
         q.put((rank, L["owned_plane_begin"] * op.plane, x.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,dim,p,n", [(2, 2, 3, (5, 200)), (3, 2, 5, (5, 240)), (4, 1, 3, (400,)),
-                                           (2, 3, 3, (3, 3, 150))])
+                                           (2, 3, 3, (3, 3, 150)), (8, 1, 7, (255,)), (8, 3, 7, (7, 8, 255)),
+                                           (6, 2, 5, (5, 150))])
 def test_slab_mass_solve_gloo(world, dim, p, n):
     """Distributed exact mass inverse by slab-local solves + one p-plane
-    exchange + the 2p x 2p interface systems (SlabMassSolve over gloo, numpy
-    test double of the device steps) == the global Kronecker inverse; the
-    library's pure-host gdm_mass_spike_eps reports the dropped coupling the
-    numpy spikes show."""
+    exchange (+ the refinement rounds of gdm_mass_spike_rounds for thin
+    slabs: C4 at 8 ranks = 32 planes at p = 7, and 25 planes at p = 5) + the
+    2p x 2p interface systems (SlabMassSolve over gloo, numpy test double of
+    the device steps) == the global Kronecker inverse to 1e-13; the library's
+    pure-host gdm_mass_spike_eps reports the dropped coupling the numpy
+    spikes show."""
     import torch.multiprocessing as mp
 
     eps = _capi.mass_spike_eps(dim, p, list(n), world)
-    assert eps < 1e-15
+    rounds = _capi.mass_spike_rounds(dim, p, list(n), world)
+    assert rounds == next(m for m in range(4) if eps ** (m + 1) <= 1e-15), (eps, rounds)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -405,7 +429,7 @@ def test_slab_mass_solve_gloo(world, dim, p, n):
     x = np.zeros_like(ref)
     for _, off, v in res:
         x[off:off + len(v)] = v
-    assert np.linalg.norm(x - ref) / np.linalg.norm(ref) < 1e-12
+    assert np.linalg.norm(x - ref) / np.linalg.norm(ref) < 1e-13
 
 
 @pytest.mark.parametrize("dim,p,n,world", [(2, 3, (5, 60), 2), (1, 5, (120,), 3), (3, 7, (7, 7, 255), 4),
@@ -425,4 +449,13 @@ def test_mass_spike_eps_matches_numpy(dim, p, n, world):
     got = _capi.mass_spike_eps(dim, p, list(n), world)
     assert got == pytest.approx(eps, rel=1e-6, abs=1e-300)
     if (dim, p, world) == (3, 7, 8):
-        assert got > 1e-15
+        # thin slabs: one refinement round (error ~ eps^2 = 4e-16)
+        assert got > 1e-15 and got ** 2 < 1e-15
+        assert _capi.mass_spike_rounds(dim, p, list(n), world) == 1
+
+
+def test_mass_spike_rounds_refuses_slabs_thinner_than_2p():
+    """8 ranks of p = 7 on 100 cells: 12-13 planes per slab < 2p, the edge
+    planes of the refinement rounds would overlap -> refused (-1)."""
+    assert _capi.mass_spike_rounds(1, 7, (100,), 8) == -1
+    assert _capi.mass_spike_rounds(3, 5, (5, 5, 511), 8) == 0

@@ -2,7 +2,7 @@
 """Stencil phase breakdown on the GPU: times the fused kernel with phases
 disabled through the diagnostic build (make -C .../csrc diag; GDM_DBG bits:
 1 consumer y-sweep, 2 consumer z-scatter, 4 producer x-sweep, 8 producer DMA,
-16 barriers).  Results are wrong by design; timing only."""
+16 barriers, 32 consumer global stores, 64 producer (A, B) LDS writes).  Results are wrong by design; timing only."""
 import os
 import sys
 
@@ -18,7 +18,8 @@ kind = sys.argv[3] if len(sys.argv) > 3 else "advection"
 op = GdmOperator(3, p, n, 0.0, 1.0, kind, params=(1.0, 0.15, -0.05) if kind == "advection" else (), device=0)
 src = torch.rand(op.n_local, dtype=torch.float64, device="cuda")
 dst = op.new_vector(local=False)
-for bits in [0, 1, 2, 3, 4, 8, 12, 15, 16, 1 | 2 | 16, 4 | 8 | 16, 31]:
+BITS = [int(b) for b in os.environ.get("GDM_DIAG_BITS", "0,1,2,3,4,8,12,15,16,19,28,31").split(",")]
+for bits in BITS:
     os.environ["GDM_DBG"] = str(bits)
     op.time_op(0, src, dst, None, 3)
     ms = op.time_op(0, src, dst, None, 10)
