@@ -145,6 +145,21 @@ def main():
     txt = rd("prototypes/cut_poisson_01_gdm.output")
     R["cut_poisson_01"] = {"source": "prototypes/cut_poisson_01_gdm.output", "text": txt.splitlines()}
 
+    # applications/advection/tests/test_01.output: advection-convergence.cc's
+    # "parallel-ramp-degree" ConvergenceTable (two blocks, p = 3 and 5)
+    txt = rd("applications/advection/tests/test_01.output")
+    header, rows = None, []
+    for line in txt.splitlines():
+        s = line.split()
+        if not s:
+            continue
+        if s[0] == "fe_degree":
+            header = s
+        else:
+            rows.append([int(s[0]), float(s[1]), int(s[2])] + [float(x) for x in s[3:]])
+    R["advection_test_01"] = {"source": "applications/advection/tests/test_01.output", "columns": header,
+                              "rows": rows, "text": txt.splitlines()}
+
     with open(os.path.join(HERE, "reference_outputs.json"), "w") as f:
         json.dump(R, f, indent=1)
     print("wrote", os.listdir(HERE))
