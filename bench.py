@@ -186,6 +186,57 @@ def cpu_baseline(p, n_cells, threads):
     }
 
 
+FP64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak (MI355X_MICROARCH.md chip table; FMA = 2 flop)
+
+
+def c4_wave_stage(steps=10):
+    """BASELINE config C4 on one GPU: applications/wave wave-rk, p = 7, 256^3
+    vertices on [-1.21, 1.21]^3 (wave/problem.h:280-346): the stiffness
+    compute_rhs (wave/stiffness.h:151-181), the exact mass inverse and one
+    device-resident RK4 stage (WaveProblem.step / 4), HIP events on the
+    operator stream.  The p = 7 stencil is FP64-ALU-bound: 105 FMA per DoF
+    (x: 15 + 15, y: 15 + 30, z: 15 + 15) = 210 flop/DoF, reported against the
+    78.6 TF/s FP64 vector peak; its HBM figure is 16 B/DoF."""
+    import torch
+    from gdm_amd import GdmOperator, WaveProblem
+
+    n, p = 255, 7
+    op = GdmOperator(3, p, n, -1.21, 1.21, "wave")
+    N = op.n_owned
+    gen = torch.Generator(device="cuda").manual_seed(20251011)
+    u = torch.rand(N, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+    v = op.new_vector(False)
+    op.time_op(0, u, v, None, 3)
+    st_ms = op.time_op(0, u, v, None, steps)
+    op.time_op(2, v, u, None, 2)
+    ms_ms = op.time_op(2, v, u, None, steps)
+    prob = WaveProblem(op)
+    prob.u.copy_(u)
+    prob.step(0.0, 1e-4)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for i in range(3):
+        prob.step(i * 1e-4, 1e-4)
+    e1.record()
+    torch.cuda.synchronize()
+    stage = e0.elapsed_time(e1) / 12.0
+    flops = 210.0 * N
+    out = {
+        "workload": "3D wave GDM p=7, 256^3 vertices (16.8 M DoFs), wave-rk",
+        "stencil_ms": st_ms,
+        "stencil_fp64_tflops": flops / (st_ms * 1e-3) / 1e12,
+        "stencil_valu_frac": flops / (st_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFS,
+        "stencil_hbm_frac": BYTES_PER_DOF * N / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "mass_solve_ms": ms_ms,
+        "rk4_stage_ms": stage,
+        "dof_updates_per_s": N / (st_ms * 1e-3),
+    }
+    del prob, op, u, v
+    torch.cuda.empty_cache()
+    return out
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -344,6 +395,9 @@ def main():
             torch.cuda.synchronize()
             stage_ms = e0.elapsed_time(e1) / 12.0
             del prob
+    c4 = None
+    if world == 1 and not args.metric_only:
+        c4 = c4_wave_stage()
     traffic = None
     if world == 1 and str(args.pmc) == "1" and not args.metric_only:
         traffic = pmc_traffic(args)
@@ -391,6 +445,7 @@ def main():
             "mass_solve": mass,
         },
         "rk4_stage_ms": stage_ms,
+        "c4_wave": c4,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -2016,5 +2016,157 @@ int gdm_cut_poisson_destroy(gdm_cut_system *S) {
   return GDM_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Cut-cell advection (include/gdm_hip.h): host assembly of the corrections
+// (gdm_cut_advection.cpp), the uncut stencil of the box, device CSR products
+// and the banded mass solve (gdm_band.hip).
+// ---------------------------------------------------------------------------
+struct gdm_cut_adv_system;
+int gdmh_cut_adv_create(int p, int n_sub, double lo, double hi, const double *level_set, const double *advection,
+                        double gamma_A, double gamma_M, gdm_cut_adv_system **out, char *err, size_t err_len);
+void gdmh_cut_adv_info(const gdm_cut_adv_system *S, int64_t *n_dofs, int64_t *n_bc, int64_t *cells,
+                       int64_t *bandwidth);
+void gdmh_cut_adv_arrays(const gdm_cut_adv_system *S, const int64_t **c_rp, const uint32_t **c_ci,
+                         const double **c_v, const int64_t **f_rp, const uint32_t **f_ci, const double **f_v,
+                         const double **bc_xy, const double **lband);
+void gdmh_cut_adv_destroy(gdm_cut_adv_system *S);
+hipError_t gdmk_launch_csr_accum(int64_t n_rows, const int64_t *rp, const uint32_t *ci, const double *v,
+                                 const double *x, double *y, hipStream_t st);
+hipError_t gdmk_launch_band_solve(int64_t n, int64_t bw, const double *L, double *x, hipStream_t st);
+
 }  // extern "C"
 
+struct gdm_cut_advection {
+  gdm_cut_adv_system *host = nullptr;
+  gdm_op *op = nullptr;
+  int64_t n_dofs = 0, n_bc = 0, bw = 0, cells[3] = {0, 0, 0};
+  int64_t *c_rp = nullptr, *f_rp = nullptr;
+  uint32_t *c_ci = nullptr, *f_ci = nullptr;
+  double *c_v = nullptr, *f_v = nullptr, *lband = nullptr;
+  std::vector<double> bc_xy;
+  void release() {
+    for (void *q : {(void *)c_rp, (void *)f_rp, (void *)c_ci, (void *)f_ci, (void *)c_v, (void *)f_v, (void *)lband})
+      if (q) (void)hipFree(q);
+    c_rp = f_rp = nullptr;
+    c_ci = f_ci = nullptr;
+    c_v = f_v = lband = nullptr;
+    if (op) gdm_op_destroy(op);
+    op = nullptr;
+    if (host) gdmh_cut_adv_destroy(host);
+    host = nullptr;
+  }
+};
+
+extern "C" {
+
+int gdm_cut_advection_create(int fe_degree, int n_subdivisions, double left, double right, const double *level_set,
+                             const double *advection, double ghost_parameter_A, double ghost_parameter_M,
+                             int device, gdm_cut_advection **out) {
+  if (!out || !level_set || !advection) return fail(GDM_ERR_ARG, "NULL argument");
+  *out = nullptr;
+  GDM_GUARD_BEGIN
+  auto *c = new gdm_cut_advection();
+  try {
+    char err[256] = {0};
+    if (gdmh_cut_adv_create(fe_degree, n_subdivisions, left, right, level_set, advection, ghost_parameter_A,
+                            ghost_parameter_M, &c->host, err, sizeof(err)) != 0) {
+      delete c;
+      return fail(GDM_ERR_ARG, err);
+    }
+    // the uncut box operator S: 2D advection with the same a (stencil + outflow traces)
+    gdm_mesh_desc m{};
+    m.dim = 2;
+    m.fe_degree = fe_degree;
+    m.n_subdivisions[0] = m.n_subdivisions[1] = n_subdivisions;
+    m.n_subdivisions[2] = 1;
+    m.lo[0] = m.lo[1] = left;
+    m.hi[0] = m.hi[1] = right;
+    m.hi[2] = 1.0;
+    m.n_ranks = 1;
+    m.rank = 0;
+    const int rc = gdm_op_create(&m, GDM_OP_ADVECTION, advection, 2, device, &c->op);
+    if (rc != GDM_OK) {
+      c->release();
+      delete c;
+      return rc;
+    }
+    gdmh_cut_adv_info(c->host, &c->n_dofs, &c->n_bc, c->cells, &c->bw);
+    const int64_t *crp, *frp;
+    const uint32_t *cci, *fci;
+    const double *cv, *fv, *xy, *lb;
+    gdmh_cut_adv_arrays(c->host, &crp, &cci, &cv, &frp, &fci, &fv, &xy, &lb);
+    const int64_t N = c->n_dofs;
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    c->c_rp = dev_upload(std::vector<int64_t>(crp, crp + N + 1));
+    c->c_ci = dev_upload(std::vector<uint32_t>(cci, cci + crp[N]));
+    c->c_v = dev_upload(std::vector<double>(cv, cv + crp[N]));
+    c->f_rp = dev_upload(std::vector<int64_t>(frp, frp + N + 1));
+    c->f_ci = dev_upload(std::vector<uint32_t>(fci, fci + frp[N]));
+    c->f_v = dev_upload(std::vector<double>(fv, fv + frp[N]));
+    c->lband = dev_upload(std::vector<double>(lb, lb + N * (c->bw + 1)));
+    c->bc_xy.assign(xy, xy + 2 * c->n_bc);
+  } catch (...) {
+    c->release();
+    delete c;
+    throw;
+  }
+  *out = c;
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_advection_info(const gdm_cut_advection *c, int64_t *n_dofs, int64_t *n_bc_points, int64_t *cells,
+                           int64_t *mass_bandwidth) {
+  if (!c || !n_dofs || !n_bc_points || !cells || !mass_bandwidth) return fail(GDM_ERR_ARG, "NULL argument");
+  *n_dofs = c->n_dofs;
+  *n_bc_points = c->n_bc;
+  for (int k = 0; k < 3; ++k) cells[k] = c->cells[k];
+  *mass_bandwidth = c->bw;
+  return GDM_OK;
+}
+
+int gdm_cut_advection_bc_points(const gdm_cut_advection *c, double *xy_host) {
+  if (!c || (c->n_bc > 0 && !xy_host)) return fail(GDM_ERR_ARG, "NULL argument");
+  std::copy(c->bc_xy.begin(), c->bc_xy.end(), xy_host);
+  return GDM_OK;
+}
+
+int gdm_cut_advection_op(gdm_cut_advection *c, gdm_op **op) {
+  if (!c || !op) return fail(GDM_ERR_ARG, "NULL argument");
+  *op = c->op;
+  return GDM_OK;
+}
+
+int gdm_cut_advection_compute_rhs(gdm_cut_advection *c, const double *u, const double *bc, double *rhs) {
+  if (!c || !u || !rhs || (c->n_bc > 0 && !bc)) return fail(GDM_ERR_ARG, "NULL argument");
+  if (u == rhs) return fail(GDM_ERR_ARG, "u and rhs must be distinct");
+  const int rc = gdm_apply(c->op, u, rhs, nullptr);  // S u (no inflow data)
+  if (rc != GDM_OK) return rc;
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  hip_check(gdmk_launch_csr_accum(c->n_dofs, c->c_rp, c->c_ci, c->c_v, u, rhs, c->op->stream), "cut correction");
+  if (c->n_bc > 0)
+    hip_check(gdmk_launch_csr_accum(c->n_dofs, c->f_rp, c->f_ci, c->f_v, bc, rhs, c->op->stream), "inflow data");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_advection_mass_solve(gdm_cut_advection *c, const double *rhs, double *x) {
+  if (!c || !rhs || !x) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  if (x != rhs)
+    hip_check(hipMemcpyAsync(x, rhs, sizeof(double) * c->n_dofs, hipMemcpyDeviceToDevice, c->op->stream), "copy");
+  hip_check(gdmk_launch_band_solve(c->n_dofs, c->bw, c->lband, x, c->op->stream), "band solve");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_advection_destroy(gdm_cut_advection *c) {
+  if (!c) return GDM_OK;
+  c->release();
+  delete c;
+  return GDM_OK;
+}
+
+}  // extern "C"

@@ -31,32 +31,10 @@
 #include <stdexcept>
 #include <vector>
 
+#include "gdm_cut.h"
 #include "gdm_setup.h"
 
 namespace gdm {
-namespace {
-
-enum { INSIDE = -1, INTERSECTED = 0, OUTSIDE = 1 };
-
-struct Bilinear {
-  double a, b, c, d;  // f(s, t) = a + b s + c t + d s t on the unit square
-  double operator()(double s, double t) const { return a + b * s + c * t + d * s * t; }
-  double gs(double t) const { return b + d * t; }
-  double gt(double s) const { return c + d * s; }
-};
-
-struct QPoint {
-  double s, t, w;
-};
-struct SPoint {
-  double s, t, w, nx, ny;
-};
-
-// root in (0, 1) of the linear function with values f0 at 0 and f1 at 1, or -1
-double linear_root(double f0, double f1) {
-  if ((f0 < 0.0 && 0.0 < f1) || (f1 < 0.0 && 0.0 < f0)) return f0 / (f0 - f1);
-  return -1.0;
-}
 
 // deal.II QuadratureGenerator on the unit box for one bilinear level set
 void saye_unit(const Bilinear &f, const std::vector<double> &qx, const std::vector<double> &qw,
@@ -134,7 +112,6 @@ void saye_unit(const Bilinear &f, const std::vector<double> &qx, const std::vect
   }
 }
 
-}  // namespace
 }  // namespace gdm
 
 struct gdm_cut_system {
@@ -151,18 +128,6 @@ struct gdm_cut_system {
 namespace {
 
 using namespace gdm;
-
-struct Shapes {
-  // values / reference derivatives of the p+1 1D shapes at a point
-  double v[16], d[16];
-};
-
-void shapes_1d(int p, int cat, double x, Shapes &out) {
-  for (int i = 0; i <= p; ++i) {
-    out.v[i] = shape_1d(p, cat, i, x, 0);
-    out.d[i] = shape_1d(p, cat, i, x, 1);
-  }
-}
 
 // inside / surface quadrature of cell (cx, cy) in reference coordinates (weights in reference measure)
 void cell_quadrature(const gdm_cut_system &S, int cx, int cy, const std::vector<double> &qx,

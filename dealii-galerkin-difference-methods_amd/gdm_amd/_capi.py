@@ -169,6 +169,13 @@ def load():
         "gdm_cut_poisson_solve": [P, P, d, d, i32, P, ctypes.POINTER(i32), ctypes.POINTER(d)],
         "gdm_cut_poisson_l2_error": [P, P, ctypes.POINTER(d)],
         "gdm_cut_poisson_destroy": [P],
+        "gdm_cut_advection_create": [i32, i32, d, d, P, P, d, d, i32, ctypes.POINTER(P)],
+        "gdm_cut_advection_info": [P, ctypes.POINTER(i64), ctypes.POINTER(i64), P, ctypes.POINTER(i64)],
+        "gdm_cut_advection_bc_points": [P, P],
+        "gdm_cut_advection_op": [P, ctypes.POINTER(P)],
+        "gdm_cut_advection_compute_rhs": [P, P, P, P],
+        "gdm_cut_advection_mass_solve": [P, P, P],
+        "gdm_cut_advection_destroy": [P],
     }
     for name, args in sig.items():
         fn = getattr(L, name)

@@ -416,6 +416,51 @@ int gdm_cut_poisson_solve(const gdm_cut_system *S, gdm_csr *A, double rel_tol, d
 int gdm_cut_poisson_l2_error(const gdm_cut_system *S, const double *u_host, double *err);
 int gdm_cut_poisson_destroy(gdm_cut_system *S);
 
+/* ------------------------------------------------------------------------
+ * Cut-cell advection (applications/advection, non-composite,
+ * alpha = 0, 2D): the device compute_rhs / mass solve of the reference's
+ * advection application on a mesh cut by an FE_Q(1) level set.
+ *
+ *   compute_rhs   rhs = S u + C u + F bc  (advection/stiffness.h:196-606):
+ *                 S = the uncut fused Kronecker stencil of the box (the
+ *                 advection operator of gdm_op_create with the box outflow
+ *                 traces, no inflow data), C = the cut correction (cut
+ *                 volume and box-face terms of every cell that is not fully
+ *                 inside minus the full ones S applies, outflow part of the
+ *                 cut-surface term (II) :420-471, ghost penalty
+ *                 -0.5 gamma_A h^2 [d_n v][d_n u] (IV) :534-598), F = the
+ *                 inflow data of (II) and (III) :473-532 (one column per
+ *                 stage boundary point); C and F assembled on the host
+ *                 (csrc/gdm_cut_advection.cpp), device CSR products.
+ *   mass_solve    x = M_cut^-1 rhs exactly: banded Cholesky of the cut mass
+ *                 (v, u)_inside + 0.5 gamma_M h^3 [d_n v][d_n u], zero
+ *                 diagonals -> 1 (advection/mass.h:47-243), factored on the
+ *                 host, triangular solves on the device (the SolverDirect
+ *                 branch of advection/problem.h:262-265).  Up to 2^22 DoFs.
+ *   bc_points     the stage boundary points (x, y) in the reference's
+ *                 point_counter order (stiffness.h:40-160: per cell in
+ *                 lexicographic order, its cut-surface points, then the inside
+ *                 parts of its box faces in face order); block(0) of the
+ *                 reference's BlockVector = the caller's values at them.
+ *   op            the inner gdm_op (its stream; vector ops such as
+ *                 gdm_vec_rk_update on these vectors).
+ * level_set: the (n_sub + 1)^2 vertex values of the level set (x fastest);
+ * cells with all values < 0 are inside, all > 0 outside (MeshClassifier).
+ * u, bc, rhs, x: device pointers (n_dofs / n_bc_points doubles).
+ * ------------------------------------------------------------------------ */
+typedef struct gdm_cut_advection gdm_cut_advection;
+int gdm_cut_advection_create(int fe_degree, int n_subdivisions, double left, double right, const double *level_set,
+                             const double *advection /* [2] */, double ghost_parameter_A, double ghost_parameter_M,
+                             int device, gdm_cut_advection **out);
+/* cells[3] = inside, intersected, outside */
+int gdm_cut_advection_info(const gdm_cut_advection *c, int64_t *n_dofs, int64_t *n_bc_points, int64_t *cells,
+                           int64_t *mass_bandwidth);
+int gdm_cut_advection_bc_points(const gdm_cut_advection *c, double *xy_host /* [n_bc_points][2] */);
+int gdm_cut_advection_op(gdm_cut_advection *c, gdm_op **op);
+int gdm_cut_advection_compute_rhs(gdm_cut_advection *c, const double *u, const double *bc, double *rhs);
+int gdm_cut_advection_mass_solve(gdm_cut_advection *c, const double *rhs, double *x);
+int gdm_cut_advection_destroy(gdm_cut_advection *c);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,4 +13,4 @@ F="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -Wno-unused-function -DGDM_ONLY_P=
 /opt/rocm/bin/hipcc $F -c $C/gdm_kernels.hip -o $O/kernels.o &&
 g++ -O3 -std=c++17 -fPIC -c $C/gdm_setup.cpp -o $O/setup.o &&
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libgdm_hip.so $O/capi.o $O/kernels.o $O/setup.o \
-  $B/gdm_csr.o $B/gdm_mass.o $B/gdm_rk.o $B/gdm_post.o $B/gdm_cut.o && echo "built $O"
+  $B/gdm_csr.o $B/gdm_mass.o $B/gdm_rk.o $B/gdm_post.o $B/gdm_cut.o $B/gdm_cut_advection.o $B/gdm_band.o && echo "built $O"
