@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--kind", default="advection", choices=["advection", "wave", "mass"])
     ap.add_argument("--strong", action="store_true", help="(default for N > 1) fixed 512^3 global grid")
     ap.add_argument("--weak", action="store_true", help="one 512-plane slab per GPU instead of a fixed global grid")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0: min(16, cpu_count))")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0: min(16, nproc))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cells", type=int, default=24, help="cells per direction of the CPU-baseline sample")
     ap.add_argument("--pmc", default=os.environ.get("GDM_BENCH_PMC", "1"), help="collect HBM PMC traffic (1/0)")
@@ -166,6 +166,7 @@ def cpu_baseline(p, n_cells, threads):
         "unit": "DoF-updates/s",
         "cores": threads,
         "cores_visible": os.cpu_count(),
+        "cores_nproc": _nproc(),
         "kind": "port",
         "cpu": _cpu_model(),
         "sample": "3D p=%d advection compute_rhs, reference per-cell algorithm (oracle/gdm_oracle.c), %d^3 cells = "
@@ -235,6 +236,13 @@ def c4_wave_stage(steps=10):
     del prob, op, u, v
     torch.cuda.empty_cache()
     return out
+
+
+def _nproc():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
 
 
 def _cpu_model():
@@ -404,8 +412,9 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not args.metric_only:
         try:
-            # the box allots 16 host CPUs per GPU (os.cpu_count() shows the whole machine there)
-            cpu = cpu_baseline(p, args.cpu_cells, args.cpu_threads or min(16, os.cpu_count() or 1))
+            # every CPU this process may run on (nproc = the affinity mask), capped at the 16 host CPUs the
+            # GPU box allots per GPU (os.cpu_count() shows the whole machine there)
+            cpu = cpu_baseline(p, args.cpu_cells, args.cpu_threads or min(16, _nproc()))
         except Exception as e:  # the baseline never blocks the GPU line
             cpu = {"value": None, "error": str(e)}
     out = {

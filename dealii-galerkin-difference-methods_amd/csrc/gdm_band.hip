@@ -21,6 +21,13 @@ __global__ void __launch_bounds__(256) csr_accum_kernel(int64_t n_rows, const in
   }
 }
 
+// y[rows[k]] = 0
+__global__ void __launch_bounds__(256) zero_rows_kernel(int64_t n, const int64_t *__restrict__ rows,
+                                                        double *__restrict__ y) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+    y[rows[k]] = 0.0;
+}
+
 // x <- (L L^T)^-1 x, L banded lower triangular with half-bandwidth bw,
 // row form L[i * (bw + 1) + k] = L(i, i - bw + k).  One workgroup: the rows
 // are sequential, each row's bw-long dot product is spread over the block
@@ -71,6 +78,13 @@ extern "C" hipError_t gdmk_launch_csr_accum(int64_t n_rows, const int64_t *rp, c
   if (n_rows <= 0) return hipSuccess;
   const int64_t blocks = (n_rows + 255) / 256 < 4096 ? (n_rows + 255) / 256 : 4096;
   hipLaunchKernelGGL(gdmk::csr_accum_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n_rows, rp, ci, v, x, y);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gdmk_launch_zero_rows(int64_t n, const int64_t *rows, double *y, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(gdmk::zero_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n, rows, y);
   return hipGetLastError();
 }
 

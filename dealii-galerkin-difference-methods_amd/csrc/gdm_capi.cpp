@@ -782,6 +782,7 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
 void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
                           hipStream_t st = nullptr) {
   if (op->kind != GDM_OP_ADVECTION) return;
+  gdmk::Face2Set s2{};
   for (const Face &F : op->faces) {
     if (F.scale == 0.0) continue;
     gdmk::FaceArgs fa{};
@@ -812,8 +813,27 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     fa.stride0 = F.t0.stride;
     fa.stride1 = F.t1.stride;
     fa.scale = F.scale;
-    fa.phase = phase;
-    hip_check(gdmk_launch_face(fa, phase == 1 && st ? st : op->stream), "face launch");
+    fa.phase = 1;  // step 1 only: step 2 of all faces is one launch below
+    if (phase != 2) hip_check(gdmk_launch_face(fa, phase == 1 && st ? st : op->stream), "face launch");
+    if (phase != 1 && fa.i0_end > fa.i0_begin && fa.i1_end > fa.i1_begin && fa.Q1 > 0) {
+      gdmk::Face2 &g = s2.f[s2.nf++];
+      g.T = fa.T;
+      g.qs1 = fa.qs1;
+      g.qc1 = fa.qc1;
+      g.w1 = fa.w1;
+      g.n0 = fa.i0_end - fa.i0_begin;
+      g.i1_begin = fa.i1_begin;
+      g.i1_end = fa.i1_end;
+      g.wmax1 = fa.wmax1;
+      g.base = fa.base;
+      g.stride0 = fa.stride0;
+      g.stride1 = fa.stride1;
+      g.scale = fa.scale;
+    }
+  }
+  if (phase != 1 && s2.nf > 0) {
+    for (int k = 0; k < s2.nf; ++k) s2.f[k].shared_edges = s2.nf > 1;
+    hip_check(gdmk_launch_face_step2_all(s2, dst_owned, op->stream), "face step 2");
   }
 }
 
@@ -2029,7 +2049,9 @@ void gdmh_cut_adv_info(const gdm_cut_adv_system *S, int64_t *n_dofs, int64_t *n_
 void gdmh_cut_adv_arrays(const gdm_cut_adv_system *S, const int64_t **c_rp, const uint32_t **c_ci,
                          const double **c_v, const int64_t **f_rp, const uint32_t **f_ci, const double **f_v,
                          const double **bc_xy, const double **lband);
+void gdmh_cut_adv_zero_rows(const gdm_cut_adv_system *S, const int64_t **rows, int64_t *n);
 void gdmh_cut_adv_destroy(gdm_cut_adv_system *S);
+hipError_t gdmk_launch_zero_rows(int64_t n, const int64_t *rows, double *y, hipStream_t st);
 hipError_t gdmk_launch_csr_accum(int64_t n_rows, const int64_t *rp, const uint32_t *ci, const double *v,
                                  const double *x, double *y, hipStream_t st);
 hipError_t gdmk_launch_band_solve(int64_t n, int64_t bw, const double *L, double *x, hipStream_t st);
@@ -2040,13 +2062,15 @@ struct gdm_cut_advection {
   gdm_cut_adv_system *host = nullptr;
   gdm_op *op = nullptr;
   int64_t n_dofs = 0, n_bc = 0, bw = 0, cells[3] = {0, 0, 0};
-  int64_t *c_rp = nullptr, *f_rp = nullptr;
+  int64_t *c_rp = nullptr, *f_rp = nullptr, *zrows = nullptr, n_zrows = 0;
   uint32_t *c_ci = nullptr, *f_ci = nullptr;
   double *c_v = nullptr, *f_v = nullptr, *lband = nullptr;
   std::vector<double> bc_xy;
   void release() {
-    for (void *q : {(void *)c_rp, (void *)f_rp, (void *)c_ci, (void *)f_ci, (void *)c_v, (void *)f_v, (void *)lband})
+    for (void *q : {(void *)c_rp, (void *)f_rp, (void *)c_ci, (void *)f_ci, (void *)c_v, (void *)f_v, (void *)lband,
+                    (void *)zrows})
       if (q) (void)hipFree(q);
+    zrows = nullptr;
     c_rp = f_rp = nullptr;
     c_ci = f_ci = nullptr;
     c_v = f_v = lband = nullptr;
@@ -2104,6 +2128,9 @@ int gdm_cut_advection_create(int fe_degree, int n_subdivisions, double left, dou
     c->f_ci = dev_upload(std::vector<uint32_t>(fci, fci + frp[N]));
     c->f_v = dev_upload(std::vector<double>(fv, fv + frp[N]));
     c->lband = dev_upload(std::vector<double>(lb, lb + N * (c->bw + 1)));
+    const int64_t *zr;
+    gdmh_cut_adv_zero_rows(c->host, &zr, &c->n_zrows);
+    if (c->n_zrows > 0) c->zrows = dev_upload(std::vector<int64_t>(zr, zr + c->n_zrows));
     c->bc_xy.assign(xy, xy + 2 * c->n_bc);
   } catch (...) {
     c->release();
@@ -2144,6 +2171,7 @@ int gdm_cut_advection_compute_rhs(gdm_cut_advection *c, const double *u, const d
   if (rc != GDM_OK) return rc;
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  hip_check(gdmk_launch_zero_rows(c->n_zrows, c->zrows, rhs, c->op->stream), "cut rows");
   hip_check(gdmk_launch_csr_accum(c->n_dofs, c->c_rp, c->c_ci, c->c_v, u, rhs, c->op->stream), "cut correction");
   if (c->n_bc > 0)
     hip_check(gdmk_launch_csr_accum(c->n_dofs, c->f_rp, c->f_ci, c->f_v, bc, rhs, c->op->stream), "inflow data");
@@ -2163,6 +2191,262 @@ int gdm_cut_advection_mass_solve(gdm_cut_advection *c, const double *rhs, double
 }
 
 int gdm_cut_advection_destroy(gdm_cut_advection *c) {
+  if (!c) return GDM_OK;
+  c->release();
+  delete c;
+  return GDM_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Cut-cell wave / heat (1D; host assembly csrc/gdm_cut_wave.cpp)
+// ---------------------------------------------------------------------------
+struct gdm_cut_wave_system;
+extern "C" {
+int gdmh_cut_wave_create(int p, int n_sub, double lo, double hi, int ls_degree, const double *ls_values,
+                         double gamma_M, double gamma_A, double nitsche, gdm_cut_wave_system **out, char *err,
+                         size_t err_len);
+void gdmh_cut_wave_info(const gdm_cut_wave_system *S, int64_t *n_dofs, int64_t *n_quad, int64_t *n_surface,
+                        int64_t *cells);
+void gdmh_cut_wave_csr(const gdm_cut_wave_system *S, int which, const int64_t **rp, const uint32_t **ci,
+                       const double **v);
+void gdmh_cut_wave_points(const gdm_cut_wave_system *S, const double **qx, const double **qw, const double **sx,
+                          const double **sn, const int64_t **zero_rows, int64_t *n_zero);
+void gdmh_cut_wave_destroy(gdm_cut_wave_system *S);
+int64_t gdmh_band_cholesky(int64_t n, const int64_t *rp, const uint32_t *ci, const double *v, double alpha,
+                           const int64_t *rp2, const uint32_t *ci2, const double *v2, std::vector<double> &lband);
+}
+
+namespace {
+struct DevCsr {
+  int64_t rows = 0;
+  int64_t *rp = nullptr;
+  uint32_t *ci = nullptr;
+  double *v = nullptr;
+  void upload(const gdm_cut_wave_system *S, int which, int64_t n_rows) {
+    const int64_t *hrp;
+    const uint32_t *hci;
+    const double *hv;
+    gdmh_cut_wave_csr(S, which, &hrp, &hci, &hv);
+    rows = n_rows;
+    rp = dev_upload(std::vector<int64_t>(hrp, hrp + n_rows + 1));
+    const int64_t nnz = hrp[n_rows];
+    std::vector<uint32_t> c1(std::max<int64_t>(nnz, 1), 0);  // one padding entry for an empty matrix
+    std::vector<double> v1(c1.size(), 0.0);
+    if (nnz > 0) {
+      std::copy(hci, hci + nnz, c1.begin());
+      std::copy(hv, hv + nnz, v1.begin());
+    }
+    ci = dev_upload(c1);
+    v = dev_upload(v1);
+  }
+  void release() {
+    for (void *q : {(void *)rp, (void *)ci, (void *)v})
+      if (q) (void)hipFree(q);
+    rp = nullptr;
+    ci = nullptr;
+    v = nullptr;
+  }
+  void accum(const double *x, double *y, hipStream_t st) const {
+    hip_check(gdmk_launch_csr_accum(rows, rp, ci, v, x, y, st), "csr accumulate");
+  }
+};
+}  // namespace
+
+struct gdm_cut_wave {
+  gdm_cut_wave_system *host = nullptr;
+  gdm_op *op = nullptr;
+  int64_t n_dofs = 0, n_quad = 0, n_surf = 0, cells[3] = {0, 0, 0};
+  DevCsr C, Ff, Fg, E, M;
+  int64_t *zrows = nullptr, n_zrows = 0;
+  int64_t bw_m = 0, bw_a = -1;
+  double *lband_m = nullptr, *lband_a = nullptr, dt_a = 0.0;
+  void release() {
+    for (DevCsr *q : {&C, &Ff, &Fg, &E, &M}) q->release();
+    for (void *q : {(void *)zrows, (void *)lband_m, (void *)lband_a})
+      if (q) (void)hipFree(q);
+    zrows = nullptr;
+    lband_m = lband_a = nullptr;
+    if (op) gdm_op_destroy(op);
+    op = nullptr;
+    if (host) gdmh_cut_wave_destroy(host);
+    host = nullptr;
+  }
+};
+
+extern "C" {
+
+int gdm_cut_wave_create(int fe_degree, int n_subdivisions, double left, double right, int ls_degree,
+                        const double *ls_values, double gamma_M, double gamma_A, double nitsche, int device,
+                        gdm_cut_wave **out) {
+  if (!out || !ls_values) return fail(GDM_ERR_ARG, "NULL argument");
+  *out = nullptr;
+  GDM_GUARD_BEGIN
+  auto *c = new gdm_cut_wave();
+  try {
+    char err[256] = {0};
+    if (gdmh_cut_wave_create(fe_degree, n_subdivisions, left, right, ls_degree, ls_values, gamma_M, gamma_A, nitsche,
+                             &c->host, err, sizeof(err)) != 0) {
+      delete c;
+      return fail(GDM_ERR_ARG, err);
+    }
+    // the uncut box operator S: 1D wave -(v', u') (no box Nitsche)
+    gdm_mesh_desc m{};
+    m.dim = 1;
+    m.fe_degree = fe_degree;
+    m.n_subdivisions[0] = n_subdivisions;
+    m.n_subdivisions[1] = m.n_subdivisions[2] = 1;
+    m.lo[0] = left;
+    m.hi[0] = right;
+    m.hi[1] = m.hi[2] = 1.0;
+    m.n_ranks = 1;
+    m.rank = 0;
+    const int rc = gdm_op_create(&m, GDM_OP_WAVE, nullptr, 0, device, &c->op);
+    if (rc != GDM_OK) {
+      c->release();
+      delete c;
+      return rc;
+    }
+    gdmh_cut_wave_info(c->host, &c->n_dofs, &c->n_quad, &c->n_surf, c->cells);
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    c->C.upload(c->host, 0, c->n_dofs);
+    c->Ff.upload(c->host, 1, c->n_dofs);
+    c->Fg.upload(c->host, 2, c->n_dofs);
+    c->E.upload(c->host, 3, c->n_quad);
+    c->M.upload(c->host, 4, c->n_dofs);
+    const double *qx, *qw, *sx, *sn;
+    const int64_t *zr;
+    gdmh_cut_wave_points(c->host, &qx, &qw, &sx, &sn, &zr, &c->n_zrows);
+    if (c->n_zrows > 0) c->zrows = dev_upload(std::vector<int64_t>(zr, zr + c->n_zrows));
+    const int64_t *rp;
+    const uint32_t *ci;
+    const double *v;
+    gdmh_cut_wave_csr(c->host, 4, &rp, &ci, &v);
+    std::vector<double> lb;
+    c->bw_m = gdmh_band_cholesky(c->n_dofs, rp, ci, v, 0.0, nullptr, nullptr, nullptr, lb);
+    if (c->bw_m < 0) throw std::runtime_error("cut wave: mass matrix not positive definite");
+    c->lband_m = dev_upload(lb);
+  } catch (...) {
+    c->release();
+    delete c;
+    throw;
+  }
+  *out = c;
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_wave_info(const gdm_cut_wave *c, int64_t *n_dofs, int64_t *n_quad, int64_t *n_surface, int64_t *cells) {
+  if (!c || !n_dofs || !n_quad || !n_surface || !cells) return fail(GDM_ERR_ARG, "NULL argument");
+  *n_dofs = c->n_dofs;
+  *n_quad = c->n_quad;
+  *n_surface = c->n_surf;
+  for (int k = 0; k < 3; ++k) cells[k] = c->cells[k];
+  return GDM_OK;
+}
+
+int gdm_cut_wave_points(const gdm_cut_wave *c, double *qx, double *qw, double *sx, double *sn) {
+  if (!c) return fail(GDM_ERR_ARG, "NULL argument");
+  const double *hqx, *hqw, *hsx, *hsn;
+  const int64_t *zr;
+  int64_t nz;
+  gdmh_cut_wave_points(c->host, &hqx, &hqw, &hsx, &hsn, &zr, &nz);
+  if (qx) std::copy(hqx, hqx + c->n_quad, qx);
+  if (qw) std::copy(hqw, hqw + c->n_quad, qw);
+  if (sx) std::copy(hsx, hsx + c->n_surf, sx);
+  if (sn) std::copy(hsn, hsn + c->n_surf, sn);
+  return GDM_OK;
+}
+
+int gdm_cut_wave_op(gdm_cut_wave *c, gdm_op **op) {
+  if (!c || !op) return fail(GDM_ERR_ARG, "NULL argument");
+  *op = c->op;
+  return GDM_OK;
+}
+
+int gdm_cut_wave_compute_rhs(gdm_cut_wave *c, const double *u, const double *fq, const double *gs, double *rhs) {
+  if (!c || !rhs) return fail(GDM_ERR_ARG, "NULL argument");
+  if (u == rhs) return fail(GDM_ERR_ARG, "u and rhs must be distinct");
+  if (u) {
+    const int rc = gdm_apply(c->op, u, rhs, nullptr);  // S u
+    if (rc != GDM_OK) return rc;
+  }
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  hipStream_t st = c->op->stream;
+  if (u) {
+    hip_check(gdmk_launch_zero_rows(c->n_zrows, c->zrows, rhs, st), "cut rows");
+    c->C.accum(u, rhs, st);
+  } else {
+    hip_check(gdmk_launch_zero(c->n_dofs, rhs, st), "zero");
+  }
+  if (fq && c->n_quad > 0) c->Ff.accum(fq, rhs, st);
+  if (gs && c->n_surf > 0) c->Fg.accum(gs, rhs, st);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_wave_mass_apply(gdm_cut_wave *c, const double *u, double *out) {
+  if (!c || !u || !out || u == out) return fail(GDM_ERR_ARG, "NULL or aliased argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  hip_check(gdmk_launch_zero(c->n_dofs, out, c->op->stream), "zero");
+  c->M.accum(u, out, c->op->stream);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_wave_mass_solve(gdm_cut_wave *c, const double *rhs, double *x) {
+  if (!c || !rhs || !x) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  if (x != rhs)
+    hip_check(hipMemcpyAsync(x, rhs, sizeof(double) * c->n_dofs, hipMemcpyDeviceToDevice, c->op->stream), "copy");
+  hip_check(gdmk_launch_band_solve(c->n_dofs, c->bw_m, c->lband_m, x, c->op->stream), "band solve");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_wave_system_solve(gdm_cut_wave *c, double dt, const double *rhs, double *x) {
+  if (!c || !rhs || !x) return fail(GDM_ERR_ARG, "NULL argument");
+  if (!(dt > 0.0)) return fail(GDM_ERR_ARG, "gdm_cut_wave_system_solve: dt must be positive");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  if (c->bw_a < 0 || dt != c->dt_a) {
+    const int64_t *rp, *rp2;
+    const uint32_t *ci, *ci2;
+    const double *v, *v2;
+    gdmh_cut_wave_csr(c->host, 4, &rp, &ci, &v);
+    gdmh_cut_wave_csr(c->host, 5, &rp2, &ci2, &v2);
+    std::vector<double> lb;
+    const int64_t bw = gdmh_band_cholesky(c->n_dofs, rp, ci, v, dt, rp2, ci2, v2, lb);
+    if (bw < 0) throw std::runtime_error("cut wave: M + dt K not positive definite");
+    // the previous factor may still be read by queued solves
+    hip_check(hipStreamSynchronize(c->op->stream), "hipStreamSynchronize");
+    if (c->lband_a) (void)hipFree(c->lband_a);
+    c->lband_a = dev_upload(lb);
+    c->bw_a = bw;
+    c->dt_a = dt;
+  }
+  if (x != rhs)
+    hip_check(hipMemcpyAsync(x, rhs, sizeof(double) * c->n_dofs, hipMemcpyDeviceToDevice, c->op->stream), "copy");
+  hip_check(gdmk_launch_band_solve(c->n_dofs, c->bw_a, c->lband_a, x, c->op->stream), "band solve");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_wave_eval(gdm_cut_wave *c, const double *u, double *vals) {
+  if (!c || !u || !vals) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  hip_check(gdmk_launch_zero(c->n_quad, vals, c->op->stream), "zero");
+  c->E.accum(u, vals, c->op->stream);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_wave_destroy(gdm_cut_wave *c) {
   if (!c) return GDM_OK;
   c->release();
   delete c;

@@ -4,16 +4,21 @@
 // include/gdm_hip.h).
 //
 // The device evaluates compute_rhs (advection/stiffness.h:196-606) as
-//   rhs = S u + C u + F bc
+//   rhs = Z (S u) + C u + F bc
 // with S the uncut fused Kronecker stencil of the whole box (the advection
-// operator kind of gdm_op with the box outflow traces, no inflow data) and
-// the two sparse matrices assembled here:
-//   C = K_cut - K_box: for every cell that is not fully inside, its cut
-//       volume term (I) and cut outflow box-face term (III) minus the full
-//       cell's (I) and (III) that S applies; the outflow part of the cut
-//       surface term (II); the ghost penalty (IV), -0.5 gamma_A h^2
+// operator kind of gdm_op with the box outflow traces, no inflow data), Z the
+// projection that zeroes the rows of DoFs in the box of a cell that is not
+// fully inside (`zero_rows`), and the two sparse matrices assembled here:
+//   C = the cut operator's rows of those DoFs in full -- the volume term (I)
+//       and the outflow box-face term (III) of every inside cell, their cut
+//       versions on intersected cells, the outflow part of the cut surface
+//       term (II) -- plus the ghost penalty (IV), -0.5 gamma_A h^2
 //       [d_n v][d_n u] on interior faces with an intersected cell and a
-//       non-outside neighbour, visited from both cells (stiffness.h:534-598)
+//       non-outside neighbour, visited from both cells (stiffness.h:534-598).
+//       (A correction form C = K_cut - K_box on top of the unprojected S
+//       cancels the full-cell terms of outside / cut cells in fp64; the cut
+//       mass matrix (cond 1e12 at p = 5) amplified that rounding to 1e-3 of
+//       the surface error norms of test_01.)
 //   F = the inflow (a.n < 0) parts of (II) and (III), one column per stage
 //       boundary point, points in the reference's point_counter order (per
 //       cell: surface points, then the boundary faces; stiffness.h:40-160)
@@ -52,6 +57,7 @@ struct gdm_cut_adv_system {
   int64_t bw = 0;             // half-bandwidth of the mass factor
   std::vector<double> lband;  // [n_rows][bw + 1]: L(i, i - bw + k)
   int64_t n_inside = 0, n_intersected = 0, n_outside = 0;
+  std::vector<int64_t> zero_rows;  // rows of S u the device zeroes (C holds them in full)
   std::vector<int64_t> m_rp;  // the assembled cut mass matrix (host checks)
   std::vector<uint32_t> m_ci;
   std::vector<double> m_v;
@@ -173,6 +179,17 @@ void assemble(gdm_cut_adv_system &S) {
   std::vector<double> Kl((size_t)nd * nd), Ml((size_t)nd * nd);
   int64_t d[256], e[256];
   int64_t n_bc = 0;
+  // rows in the box of a cell that is not fully inside: C carries their whole cut row
+  std::vector<uint8_t> full_row((size_t)N * N, 0);
+  for (int cy = 0; cy < n; ++cy)
+    for (int cx = 0; cx < n; ++cx)
+      if (S.loc[(size_t)cy * n + cx] != INSIDE) {
+        dofs(cx, cy, d);
+        for (int i = 0; i < nd; ++i) full_row[(size_t)d[i]] = 1;
+      }
+  S.zero_rows.clear();
+  for (int64_t r = 0; r < (int64_t)N * N; ++r)
+    if (full_row[(size_t)r]) S.zero_rows.push_back(r);
   for (int cy = 0; cy < n; ++cy)
     for (int cx = 0; cx < n; ++cx) {
       const int loc = S.loc[(size_t)cy * n + cx];
@@ -212,48 +229,32 @@ void assemble(gdm_cut_adv_system &S) {
         S.bc_xy.push_back(S.lo + (cy + t) * h);
       };
       if (loc == OUTSIDE) {
-        ++S.n_outside;
-        volume(full_cell, -1.0, false);  // remove S's full cell (I)
-        for (int f = 0; f < 4; ++f)
-          if (at_bnd[f]) {
-            const double flux = nrm[f][0] * ax + nrm[f][1] * ay;
-            for (int q = 0; q < n1; ++q) {
-              const double s = f < 2 ? (double)f : qx[q], t = f < 2 ? qx[q] : (double)(f - 2);
-              upwind(s, t, flux, qw[q] * h, -1.0, false);  // remove S's outflow trace
-            }
-          }
+        ++S.n_outside;  // no terms (its rows are zeroed in S u and carry the cut terms of their other cells)
       } else {
         if (loc == INSIDE) {
           ++S.n_inside;
-          volume(full_cell, 0.0, true);  // (I) == S's cell term: mass only
+          volume(full_cell, 1.0, true);  // (I) == S's cell term: kept below for the full rows only
         } else {
           ++S.n_intersected;
           const double v00 = lsv(cx, cy), v10 = lsv(cx + 1, cy), v01 = lsv(cx, cy + 1), v11 = lsv(cx + 1, cy + 1);
           Bilinear fl{v00, v10 - v00, v01 - v00, v11 - v10 - v01 + v00};
           saye_unit(fl, qx, qw, ins, sur);
           volume(ins, 1.0, true);
-          volume(full_cell, -1.0, false);
           for (const SPoint &q : sur) {  // (II) cut surface
             add_point(q.s, q.t);
             upwind(q.s, q.t, q.nx * ax + q.ny * ay, q.w * h, 1.0, true);
             ++n_bc;
           }
         }
-        for (int f = 0; f < 4; ++f) {  // (III) box faces
+        for (int f = 0; f < 4; ++f) {  // (III) box faces: outflow into K, inflow into F
           if (!at_bnd[f]) continue;
           const double flux = nrm[f][0] * ax + nrm[f][1] * ay;
           face_quadrature(cx, cy, f, fq);
           for (const QPoint &q : fq) {
             add_point(q.s, q.t);
-            // inside cells: the cut face is the full face, S's trace equals it (no correction)
-            upwind(q.s, q.t, flux, q.w * h, loc == INSIDE ? 0.0 : 1.0, true);
+            upwind(q.s, q.t, flux, q.w * h, 1.0, true);
             ++n_bc;
           }
-          if (loc != INSIDE)
-            for (int q = 0; q < n1; ++q) {
-              const double s = f < 2 ? (double)f : qx[q], t = f < 2 ? qx[q] : (double)(f - 2);
-              upwind(s, t, flux, qw[q] * h, -1.0, false);
-            }
         }
         // (IV) ghost penalty on the faces to (intersected | non-outside) neighbours
         const int nb[4][2] = {{cx - 1, cy}, {cx + 1, cy}, {cx, cy - 1}, {cx, cy + 1}};
@@ -287,10 +288,14 @@ void assemble(gdm_cut_adv_system &S) {
             }
         }
       }
-      for (int i = 0; i < nd; ++i)
-        for (int j = 0; j < nd; ++j) {
-          if (Kl[(size_t)i * nd + j] != 0.0 || loc == INTERSECTED || loc == OUTSIDE) C.add(d[i], d[j], Kl[(size_t)i * nd + j]);
-          if (loc != OUTSIDE) M.add(d[i], d[j], Ml[(size_t)i * nd + j]);
+      if (loc != OUTSIDE)
+        for (int i = 0; i < nd; ++i) {
+          // inside cells: S u carries row d[i] unless it is a full row
+          const bool to_c = loc == INTERSECTED || full_row[(size_t)d[i]];
+          for (int j = 0; j < nd; ++j) {
+            if (to_c) C.add(d[i], d[j], Kl[(size_t)i * nd + j]);
+            M.add(d[i], d[j], Ml[(size_t)i * nd + j]);
+          }
         }
     }
   C.csr(S.c_rp, S.c_ci, S.c_v, false);
@@ -415,6 +420,11 @@ void gdmh_cut_adv_arrays(const gdm_cut_adv_system *S, const int64_t **c_rp, cons
   *f_v = S->f_v.data();
   *bc_xy = S->bc_xy.data();
   *lband = S->lband.data();
+}
+
+void gdmh_cut_adv_zero_rows(const gdm_cut_adv_system *S, const int64_t **rows, int64_t *n) {
+  *rows = S->zero_rows.data();
+  *n = (int64_t)S->zero_rows.size();
 }
 
 void gdmh_cut_adv_mass(const gdm_cut_adv_system *S, const int64_t **rp, const uint32_t **ci, const double **v) {

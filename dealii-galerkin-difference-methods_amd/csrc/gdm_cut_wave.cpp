@@ -1,0 +1,432 @@
+// gdm_cut_wave.cpp -- host assembly of the cut-cell parts of the 1D wave /
+// heat application (applications/wave, location "inside", no domain
+// Dirichlet data: wave-app.cc presets "wave", "heat-rk", "heat-impl" at
+// dim = 1) for the device operator of gdm_capi.cpp ("Cut-cell wave" in
+// include/gdm_hip.h).
+//
+// The mesh is a GDM line [left, right] cut by the FE_Q(k) interpolant of a
+// level set (wave/discretization.h:82-99: SignedDistance::Sphere into FE_Q(k),
+// MeshClassifier): the caller gives the interpolant's values at the k + 1
+// Gauss-Lobatto support points of every cell.  Per cell: inside (all values
+// < 0), outside (all > 0) or intersected; an intersected cell's inside part
+// is found from the roots of its interpolant (sign changes on a 64-interval
+// grid refined by bisection to machine precision) and carries QGauss(p+1) on
+// each inside sub-interval and one surface point per root (weight 1, normal
+// = sign of the interpolant's slope) -- NonMatching::FEValues in 1D.
+//
+// The device evaluates StiffnessMatrixOperator::compute_rhs
+// (wave/stiffness.h:42-407) as
+//   rhs = impl ? (Z S u + C u) : 0  +  Ff f(x_q, t)  +  Fg g(x_s, t)
+// with S the uncut 1D wave stencil of the box (-(v', u'), gdm_op kind wave),
+// Z zeroing the rows of DoFs in the box of a cell that is not fully inside,
+// and the sparse parts assembled here:
+//   C   those rows of -(v', u')_inside in full, the surface Nitsche terms
+//       -(-n v' u - n u' v + gamma_D / h v u) (stiffness.h:205-259) of the
+//       cut cells, and the ghost penalty -0.5 gamma_A h [v'][u'] (h^1 in the
+//       right-hand side, stiffness.h:386-392) on the faces of intersected
+//       cells with a non-outside neighbour, visited from both cells;
+//   Ff  (v, f): column q = the inside quadrature point q (JxW folded in);
+//   Fg  the Nitsche data g (gamma_D / h v - n v'): column s = surface point s.
+// Mass (wave/mass.h:47-249): (v, u)_inside + 0.5 gamma_M h^3 [v'][u'], zero
+// diagonals -> 1; stiffness matrix of heat-impl (stiffness.h:602-800):
+// (v', u')_inside + surface Nitsche + 0.5 gamma_A h^3 [v'][u'], zero
+// diagonals -> 1.  Both are small band matrices: the mass solve and the
+// (M + dt S) solve of heat-impl are exact banded Cholesky solves (factor
+// here, triangular solves on the device), the reference's 1D solves
+// converge in 1-2 preconditioned CG steps to 1e-14 (wave_0.output).
+// E (n_quad x N): shape values at the inside quadrature points, for the
+// postprocess (problem.h:504-590).  Test oracle: oracle/cut1d.py, pinned by
+// applications/wave/tests/{wave_0,heat_0,heat_1}.output.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <stdexcept>
+#include <vector>
+
+#include "gdm_cut.h"
+#include "gdm_setup.h"
+
+struct gdm_cut_wave_system {
+  int p = 0, n = 0, k = 0;
+  double lo = 0.0, h = 0.0, gM = 0.0, gA = 0.0, nitsche = 0.0;
+  std::vector<int8_t> loc;
+  std::vector<double> qx, qw;  // inside quadrature: global x, JxW
+  std::vector<double> sx, sn;  // surface points: global x, normal
+  std::vector<int64_t> zero_rows;
+  // CSR: C [N][N], Ff [N][nq], Fg [N][ns], E [nq][N], M [N][N], S [N][N]
+  std::vector<int64_t> c_rp, ff_rp, fg_rp, e_rp, m_rp, s_rp;
+  std::vector<uint32_t> c_ci, ff_ci, fg_ci, e_ci, m_ci, s_ci;
+  std::vector<double> c_v, ff_v, fg_v, e_v, m_v, s_v;
+  int64_t cells[3] = {0, 0, 0};
+};
+
+namespace {
+
+using namespace gdm;
+
+// Gauss-Lobatto points of n >= 2 points on [0, 1] (FE_Q support points):
+// the roots of P'_{n-1} by Newton from the Chebyshev-Gauss-Lobatto guesses
+std::vector<double> gauss_lobatto(int n) {
+  std::vector<double> x(n);
+  x[0] = 0.0;
+  x[n - 1] = 1.0;
+  const int m = n - 1;
+  for (int i = 1; i < m; ++i) {
+    double t = -std::cos(M_PI * i / m);  // on [-1, 1]
+    for (int it = 0; it < 100; ++it) {
+      // P_m and its derivatives by the recurrence
+      double p0 = 1.0, p1 = t;
+      for (int j = 2; j <= m; ++j) {
+        const double p2 = ((2 * j - 1) * t * p1 - (j - 1) * p0) / j;
+        p0 = p1;
+        p1 = p2;
+      }
+      const double dp = m * (t * p1 - p0) / (t * t - 1.0);        // P'_m
+      const double d2p = (2.0 * t * dp - m * (m + 1) * p1) / (1.0 - t * t);  // P''_m
+      const double dt = dp / d2p;
+      t -= dt;
+      if (std::fabs(dt) < 1e-16) break;
+    }
+    x[i] = 0.5 * (t + 1.0);
+  }
+  std::sort(x.begin(), x.end());
+  return x;
+}
+
+// band accumulator of an N x N matrix with couplings |i - j| <= R
+struct Band1 {
+  int64_t N = 0;
+  int R = 0;
+  std::vector<double> v;
+  std::vector<uint8_t> touched;
+  void init(int64_t N_, int R_) {
+    N = N_;
+    R = R_;
+    v.assign((size_t)N * (2 * R + 1), 0.0);
+    touched.assign(v.size(), 0);
+  }
+  void add(int64_t i, int64_t j, double x) {
+    const size_t o = (size_t)i * (2 * R + 1) + (size_t)(j - i + R);
+    v[o] += x;
+    touched[o] = 1;
+  }
+  void csr(std::vector<int64_t> &rp, std::vector<uint32_t> &ci, std::vector<double> &vals, bool unit_diag) const {
+    rp.assign((size_t)N + 1, 0);
+    ci.clear();
+    vals.clear();
+    for (int64_t i = 0; i < N; ++i) {
+      for (int k = 0; k <= 2 * R; ++k) {
+        const int64_t j = i + k - R;
+        const bool diag = k == R;
+        if (j < 0 || j >= N) continue;
+        const size_t o = (size_t)i * (2 * R + 1) + (size_t)k;
+        if (!touched[o] && !(diag && unit_diag)) continue;
+        double x = v[o];
+        if (diag && unit_diag && x == 0.0) x = 1.0;
+        ci.push_back((uint32_t)j);
+        vals.push_back(x);
+      }
+      rp[(size_t)i + 1] = (int64_t)ci.size();
+    }
+  }
+};
+
+// CSR from (row, col, value) triplets, duplicates summed in insertion order
+struct Trip {
+  int64_t r, c;
+  double v;
+};
+void triplets_csr(std::vector<Trip> t, int64_t rows, std::vector<int64_t> &rp, std::vector<uint32_t> &ci,
+                  std::vector<double> &vals) {
+  std::stable_sort(t.begin(), t.end(), [](const Trip &a, const Trip &b) { return a.r != b.r ? a.r < b.r : a.c < b.c; });
+  rp.assign((size_t)rows + 1, 0);
+  ci.clear();
+  vals.clear();
+  for (size_t q = 0; q < t.size(); ++q) {
+    if (q > 0 && t[q - 1].r == t[q].r && t[q - 1].c == t[q].c) {
+      vals.back() += t[q].v;
+      continue;
+    }
+    ci.push_back((uint32_t)t[q].c);
+    vals.push_back(t[q].v);
+    ++rp[(size_t)t[q].r + 1];
+  }
+  for (int64_t r = 0; r < rows; ++r) rp[(size_t)r + 1] += rp[(size_t)r];
+}
+
+void assemble(gdm_cut_wave_system &S, const double *ls_values) {
+  const int p = S.p, n = S.n, k = S.k, n1 = p + 1;
+  const int64_t N = n + 1;
+  const double h = S.h;
+  std::vector<double> gx, gw;
+  gauss_unit(n1, gx, gw);
+  const std::vector<double> gl = gauss_lobatto(k + 1);
+  S.loc.assign(n, OUTSIDE);
+  // per cell: inside quadrature (reference s, reference weight) and surface (s, normal)
+  std::vector<std::vector<std::pair<double, double>>> cq(n), cs(n);
+  for (int c = 0; c < n; ++c) {
+    const double *vals = ls_values + (size_t)c * (k + 1);
+    bool neg = true, pos = true;
+    for (int a = 0; a <= k; ++a) {
+      neg = neg && vals[a] < 0.0;
+      pos = pos && vals[a] > 0.0;
+    }
+    auto phi = [&](double s) {
+      double r = 0.0;
+      for (int a = 0; a <= k; ++a) {
+        double la = 1.0;
+        for (int b = 0; b <= k; ++b)
+          if (b != a) la *= (s - gl[b]) / (gl[a] - gl[b]);
+        r += vals[a] * la;
+      }
+      return r;
+    };
+    if (neg) {
+      S.loc[c] = INSIDE;
+      for (int q = 0; q < n1; ++q) cq[c].push_back({gx[q], gw[q]});
+      continue;
+    }
+    if (pos) continue;
+    S.loc[c] = INTERSECTED;
+    constexpr int G = 64;
+    double pv[G + 1];
+    for (int a = 0; a <= G; ++a) pv[a] = phi((double)a / G);
+    std::vector<double> roots;
+    for (int a = 0; a < G; ++a) {
+      const double s0 = (double)a / G, s1 = (double)(a + 1) / G;
+      if (pv[a] == 0.0) {
+        roots.push_back(s0);
+      } else if (pv[a] * pv[a + 1] < 0.0) {
+        double lo = s0, hi = s1, flo = pv[a];
+        for (int it = 0; it < 200; ++it) {
+          const double mid = 0.5 * (lo + hi);
+          if (mid == lo || mid == hi) break;
+          const double fm = phi(mid);
+          if ((fm < 0.0) == (flo < 0.0)) {
+            lo = mid;
+            flo = fm;
+          } else {
+            hi = mid;
+          }
+        }
+        roots.push_back(0.5 * (lo + hi));
+      }
+    }
+    std::vector<double> pts;
+    pts.push_back(0.0);
+    pts.insert(pts.end(), roots.begin(), roots.end());
+    pts.push_back(1.0);
+    for (size_t a = 0; a + 1 < pts.size(); ++a) {
+      const double s0 = pts[a], s1 = pts[a + 1];
+      if (phi(0.5 * (s0 + s1)) < 0.0)
+        for (int q = 0; q < n1; ++q) cq[c].push_back({s0 + (s1 - s0) * gx[q], (s1 - s0) * gw[q]});
+    }
+    for (double r : roots) {
+      const double e = 1e-7;
+      const double g = phi(std::min(r + e, 1.0)) - phi(std::max(r - e, 0.0));
+      cs[c].push_back({r, g > 0.0 ? 1.0 : -1.0});
+    }
+  }
+  for (int c = 0; c < n; ++c) ++S.cells[S.loc[c] == INSIDE ? 0 : (S.loc[c] == INTERSECTED ? 1 : 2)];
+  auto cat_of = [&](int c) { return (int)category((unsigned)c, (unsigned)p, (unsigned)n); };
+  auto off_of = [&](int c) { return (int64_t)box_offset((unsigned)c, (unsigned)p, (unsigned)n); };
+  std::vector<uint8_t> full_row((size_t)N, 0);
+  for (int c = 0; c < n; ++c)
+    if (S.loc[c] != INSIDE)
+      for (int i = 0; i < n1; ++i) full_row[(size_t)(off_of(c) + i)] = 1;
+  for (int64_t r = 0; r < N; ++r)
+    if (full_row[(size_t)r]) S.zero_rows.push_back(r);
+  Band1 C, M, K;
+  C.init(N, p + 1);
+  M.init(N, p + 1);
+  K.init(N, p + 1);
+  std::vector<Trip> ff, fg, ev;
+  Shapes sh{};
+  for (int c = 0; c < n; ++c) {
+    if (S.loc[c] == OUTSIDE) continue;
+    const int cat = cat_of(c);
+    const int64_t off = off_of(c);
+    const double x0 = S.lo + c * h;
+    for (const auto &q : cq[c]) {
+      shapes_1d(p, cat, q.first, sh);
+      const double jxw = q.second * h;
+      const int64_t qi = (int64_t)S.qx.size();
+      S.qx.push_back(x0 + q.first * h);
+      S.qw.push_back(jxw);
+      for (int i = 0; i < n1; ++i) {
+        const double gi = sh.d[i] / h;
+        ff.push_back({off + i, qi, sh.v[i] * jxw});
+        ev.push_back({qi, off + i, sh.v[i]});
+        for (int j = 0; j < n1; ++j) {
+          const double gj = sh.d[j] / h;
+          if (S.loc[c] == INTERSECTED || full_row[(size_t)(off + i)]) C.add(off + i, off + j, -gi * gj * jxw);
+          M.add(off + i, off + j, sh.v[i] * sh.v[j] * jxw);
+          K.add(off + i, off + j, gi * gj * jxw);
+        }
+      }
+    }
+    for (const auto &sp : cs[c]) {
+      shapes_1d(p, cat, sp.first, sh);
+      const double nrm = sp.second, gd = S.nitsche / h;
+      const int64_t si = (int64_t)S.sx.size();
+      S.sx.push_back(x0 + sp.first * h);
+      S.sn.push_back(nrm);
+      for (int i = 0; i < n1; ++i) {
+        const double vi = sh.v[i], gi = sh.d[i] / h;
+        fg.push_back({off + i, si, gd * vi - nrm * gi});
+        for (int j = 0; j < n1; ++j) {
+          const double vj = sh.v[j], gj = sh.d[j] / h;
+          const double a = -nrm * gi * vj - nrm * vi * gj + gd * vi * vj;
+          C.add(off + i, off + j, -a);
+          K.add(off + i, off + j, a);
+        }
+      }
+    }
+  }
+  // ghost penalty faces (mass.h:86-105, stiffness.h:80-98): every face of a
+  // non-outside cell to a neighbour where one of the two is intersected and
+  // the other not outside, visited from both cells
+  for (int c = 0; c < n; ++c) {
+    if (S.loc[c] == OUTSIDE) continue;
+    for (int f = 0; f < 2; ++f) {
+      const int nb = f == 0 ? c - 1 : c + 1;
+      if (nb < 0 || nb >= n) continue;
+      const int ln = S.loc[nb];
+      if (!((S.loc[c] == INTERSECTED && ln != OUTSIDE) || (ln == INTERSECTED && S.loc[c] != OUTSIDE))) continue;
+      // [dphi/dx] at the face: from cell c minus from the neighbour, per global DoF
+      std::map<int64_t, double> jump;
+      const double sc = (double)f, sn = 1.0 - f;  // face point in c's / the neighbour's reference coordinate
+      shapes_1d(p, cat_of(c), sc, sh);
+      for (int i = 0; i < n1; ++i) jump[off_of(c) + i] += sh.d[i] / h;
+      shapes_1d(p, cat_of(nb), sn, sh);
+      for (int i = 0; i < n1; ++i) jump[off_of(nb) + i] -= sh.d[i] / h;
+      for (const auto &a : jump)
+        for (const auto &b : jump) {
+          C.add(a.first, b.first, -0.5 * S.gA * h * a.second * b.second);
+          M.add(a.first, b.first, 0.5 * S.gM * h * h * h * a.second * b.second);
+          K.add(a.first, b.first, 0.5 * S.gA * h * h * h * a.second * b.second);
+        }
+    }
+  }
+  C.csr(S.c_rp, S.c_ci, S.c_v, false);
+  M.csr(S.m_rp, S.m_ci, S.m_v, true);
+  K.csr(S.s_rp, S.s_ci, S.s_v, true);
+  triplets_csr(ff, N, S.ff_rp, S.ff_ci, S.ff_v);
+  triplets_csr(fg, N, S.fg_rp, S.fg_ci, S.fg_v);
+  triplets_csr(ev, (int64_t)S.qx.size(), S.e_rp, S.e_ci, S.e_v);
+}
+
+}  // namespace
+
+extern "C" {
+
+// banded Cholesky of a CSR SPD matrix (half-bandwidth taken from the pattern):
+// lband [n][bw + 1], L(i, i - bw + k); returns bw, or -1 if not positive definite
+int64_t gdmh_band_cholesky(int64_t n, const int64_t *rp, const uint32_t *ci, const double *v, double alpha,
+                           const int64_t *rp2, const uint32_t *ci2, const double *v2, std::vector<double> &lband);
+
+int gdmh_cut_wave_create(int p, int n_sub, double lo, double hi, int ls_degree, const double *ls_values,
+                         double gamma_M, double gamma_A, double nitsche, gdm_cut_wave_system **out, char *err,
+                         size_t err_len) {
+  try {
+    if (!out || !ls_values || p < 1 || p > 9 || p % 2 == 0 || n_sub < p || !(hi > lo) || ls_degree < 1 ||
+        ls_degree > 9)
+      throw std::invalid_argument("cut_wave: invalid arguments (p odd in [1, 9], n_sub >= p, hi > lo, 1 <= k <= 9)");
+    auto *S = new gdm_cut_wave_system();
+    S->p = p;
+    S->n = n_sub;
+    S->k = ls_degree;
+    S->lo = lo;
+    S->h = (hi - lo) / n_sub;
+    S->gM = gamma_M;
+    S->gA = gamma_A;
+    S->nitsche = nitsche;
+    try {
+      assemble(*S, ls_values);
+    } catch (...) {
+      delete S;
+      throw;
+    }
+    *out = S;
+    return 0;
+  } catch (const std::exception &e) {
+    if (err && err_len) std::snprintf(err, err_len, "%s", e.what());
+    return -1;
+  }
+}
+
+void gdmh_cut_wave_info(const gdm_cut_wave_system *S, int64_t *n_dofs, int64_t *n_quad, int64_t *n_surface,
+                        int64_t *cells) {
+  *n_dofs = S->n + 1;
+  *n_quad = (int64_t)S->qx.size();
+  *n_surface = (int64_t)S->sx.size();
+  for (int q = 0; q < 3; ++q) cells[q] = S->cells[q];
+}
+
+// which: 0 C, 1 Ff, 2 Fg, 3 E, 4 M, 5 S (heat-impl stiffness)
+void gdmh_cut_wave_csr(const gdm_cut_wave_system *S, int which, const int64_t **rp, const uint32_t **ci,
+                       const double **v) {
+  switch (which) {
+    case 0: *rp = S->c_rp.data(); *ci = S->c_ci.data(); *v = S->c_v.data(); return;
+    case 1: *rp = S->ff_rp.data(); *ci = S->ff_ci.data(); *v = S->ff_v.data(); return;
+    case 2: *rp = S->fg_rp.data(); *ci = S->fg_ci.data(); *v = S->fg_v.data(); return;
+    case 3: *rp = S->e_rp.data(); *ci = S->e_ci.data(); *v = S->e_v.data(); return;
+    case 4: *rp = S->m_rp.data(); *ci = S->m_ci.data(); *v = S->m_v.data(); return;
+    default: *rp = S->s_rp.data(); *ci = S->s_ci.data(); *v = S->s_v.data(); return;
+  }
+}
+
+void gdmh_cut_wave_points(const gdm_cut_wave_system *S, const double **qx, const double **qw, const double **sx,
+                          const double **sn, const int64_t **zero_rows, int64_t *n_zero) {
+  *qx = S->qx.data();
+  *qw = S->qw.data();
+  *sx = S->sx.data();
+  *sn = S->sn.data();
+  *zero_rows = S->zero_rows.data();
+  *n_zero = (int64_t)S->zero_rows.size();
+}
+
+void gdmh_cut_wave_destroy(gdm_cut_wave_system *S) { delete S; }
+
+int64_t gdmh_band_cholesky(int64_t n, const int64_t *rp, const uint32_t *ci, const double *v, double alpha,
+                           const int64_t *rp2, const uint32_t *ci2, const double *v2, std::vector<double> &lband) {
+  // A = M + alpha K (rp2 may be NULL: A = M)
+  int64_t bw = 0;
+  for (int64_t r = 0; r < n; ++r) {
+    for (int64_t q = rp[r]; q < rp[r + 1]; ++q) bw = std::max<int64_t>(bw, r - (int64_t)ci[q]);
+    if (rp2)
+      for (int64_t q = rp2[r]; q < rp2[r + 1]; ++q) bw = std::max<int64_t>(bw, r - (int64_t)ci2[q]);
+  }
+  const int64_t W = bw + 1;
+  std::vector<double> A((size_t)n * W, 0.0);
+  for (int64_t r = 0; r < n; ++r) {
+    for (int64_t q = rp[r]; q < rp[r + 1]; ++q)
+      if ((int64_t)ci[q] <= r) A[(size_t)r * W + (ci[q] - r + bw)] += v[q];
+    if (rp2)
+      for (int64_t q = rp2[r]; q < rp2[r + 1]; ++q)
+        if ((int64_t)ci2[q] <= r) A[(size_t)r * W + (ci2[q] - r + bw)] += alpha * v2[q];
+  }
+  lband.assign((size_t)n * W, 0.0);
+  double *L = lband.data();
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t j0 = std::max<int64_t>(0, i - bw);
+    for (int64_t j = j0; j <= i; ++j) {
+      double s = A[(size_t)i * W + (j - i + bw)];
+      const int64_t k0 = std::max(j0, j - bw);
+      const double *Li = L + (size_t)i * W - i + bw;
+      const double *Lj = L + (size_t)j * W - j + bw;
+      for (int64_t k = k0; k < j; ++k) s -= Li[k] * Lj[k];
+      if (j < i) {
+        L[(size_t)i * W + (j - i + bw)] = s / Lj[j];
+      } else {
+        if (!(s > 0.0)) return -1;
+        L[(size_t)i * W + bw] = std::sqrt(s);
+      }
+    }
+  }
+  return bw;
+}
+
+}  // extern "C"

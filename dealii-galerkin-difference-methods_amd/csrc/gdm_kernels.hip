@@ -19,6 +19,7 @@
 // per-lane registers (they differ only near the x faces).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include <cstdlib>
 
 #include "gdm_coeffs.h"
@@ -31,6 +32,14 @@
 #endif
 #ifndef GDM_PF5
 #define GDM_PF5 2
+#endif
+#ifndef GDM_R7
+#define GDM_R7 2
+#define GDM_NC7 8
+#define GDM_NP7 8
+#endif
+#ifndef GDM_PF7
+#define GDM_PF7 3
 #endif
 namespace gdmk {
 
@@ -1162,6 +1171,9 @@ __device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7
   // ZI: the host launched this kernel only on output planes whose z columns
   // are all interior -> compile-time z bands, no table reads; otherwise every
   // plane reads its column (wall columns or the interior one) from LDS
+  // (one launch for all planes, choosing the compile-time or the table z
+  // column per block of W planes, measured 1.25 vs 0.86 ms at C3: the
+  // consumer loop carries both paths; profiles/r3j/ab_zmix.txt)
   for (int zb = t.zs; zb < t.zend; zb += W)
     cblock8<0, P, R, NC, NP, BK, PF, !ZI, YW>(a, t, ybase, full, acc, zb);
 }
@@ -1421,6 +1433,26 @@ __global__ void __launch_bounds__(256) face_step2_kernel(const double *__restric
   *d += scale * s;
 }
 
+// step 2 of every inflow face in one launch (blockIdx.z = face): the faces
+// run concurrently, so the box-edge nodes two faces share take both
+// contributions by hardware fp64 atomic adds (the sum of two or three terms
+// in either order)
+__global__ void __launch_bounds__(256) face_step2_all_kernel(const Face2Set s, double *__restrict__ dst) {
+  const Face2 &f = s.f[blockIdx.z];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i1 = f.i1_begin + (int)blockIdx.y;
+  if (t >= f.n0 || i1 >= f.i1_end) return;
+  const double *w = f.w1 + (int64_t)i1 * f.wmax1;
+  const int n = f.qc1[i1], q = f.qs1[i1];
+  double acc = 0.0;
+  for (int m = 0; m < n; ++m) acc = fma(w[m], f.T[(int64_t)(q + m) * f.n0 + t], acc);
+  double *d = dst + f.base + (int64_t)t * f.stride0 + (int64_t)(i1 - f.i1_begin) * f.stride1;
+  if (f.shared_edges)
+    unsafeAtomicAdd(d, f.scale * acc);
+  else
+    *d += f.scale * acc;
+}
+
 // ---------------------------------------------------------------------------
 // BLAS-1
 // ---------------------------------------------------------------------------
@@ -1562,7 +1594,7 @@ extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, bool zint, const gdmk:
     case 5: return launch8_p<5, GDM_R5, GDM_NC5, GDM_NP5, GDM_PF5>(bk, zint, a, st);
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 7
-    case 7: return launch8_p<7, 2, 8, 8, 3>(bk, zint, a, st);
+    case 7: return launch8_p<7, GDM_R7, GDM_NC7, GDM_NP7, GDM_PF7>(bk, zint, a, st);
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 9
     case 9: return launch8_p<9, 2, 8, 8, 3>(bk, zint, a, st);
@@ -1574,7 +1606,10 @@ extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, bool zint, const gdmk:
 
 // <P, R, NC, NP>: R output rows per consumer wave, NC consumer and NP producer
 // waves -> tile 64 x (R NC)
-extern "C" int gdmk_stencil_tile_rows(int p) { return p <= 5 ? 32 : 16; }
+extern "C" int gdmk_stencil_tile_rows(int p) {
+  using namespace gdmk;
+  return p < 5 ? 32 : (p == 5 ? Geom8<5, GDM_R5, GDM_NC5, GDM_NP5, 1>::TY : (p == 7 ? Geom8<7, GDM_R7, GDM_NC7, GDM_NP7, 1>::TY : 16));
+}
 
 extern "C" void gdmk_stencil8_geom(int p, int *tile_rows, int *wgs_per_cu) {
   using namespace gdmk;
@@ -1583,7 +1618,11 @@ extern "C" void gdmk_stencil8_geom(int p, int *tile_rows, int *wgs_per_cu) {
       *tile_rows = Geom8<5, GDM_R5, GDM_NC5, GDM_NP5, 1>::TY;
       *wgs_per_cu = Geom8<5, GDM_R5, GDM_NC5, GDM_NP5, 1>::WGS;
       return;
-    case 7: case 9: *tile_rows = 16; *wgs_per_cu = 1; return;
+    case 7:
+      *tile_rows = Geom8<7, GDM_R7, GDM_NC7, GDM_NP7, 1>::TY;
+      *wgs_per_cu = Geom8<7, GDM_R7, GDM_NC7, GDM_NP7, 1>::WGS;
+      return;
+    case 9: *tile_rows = 16; *wgs_per_cu = 1; return;
     default: *tile_rows = 32; *wgs_per_cu = 1; return;
   }
 }
@@ -1675,6 +1714,18 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
   if (f.phase != 1)
     hipLaunchKernelGGL(face_step2_kernel, g2, b, 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1,
                        f.dst, f.base, f.stride0, f.stride1, f.scale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gdmk_launch_face_step2_all(const gdmk::Face2Set &s, double *dst, hipStream_t st) {
+  using namespace gdmk;
+  int gx = 0, gy = 0;
+  for (int k = 0; k < s.nf; ++k) {
+    gx = std::max(gx, (s.f[k].n0 + 255) / 256);
+    gy = std::max(gy, s.f[k].i1_end - s.f[k].i1_begin);
+  }
+  if (s.nf == 0 || gx == 0 || gy == 0) return hipSuccess;
+  hipLaunchKernelGGL(face_step2_all_kernel, dim3(gx, gy, s.nf), dim3(256), 0, st, s, dst);
   return hipGetLastError();
 }
 

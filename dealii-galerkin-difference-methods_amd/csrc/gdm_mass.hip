@@ -586,7 +586,10 @@ __global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel
 // ds_read_b128 of a lane's own row) one chunk ahead into tile c % 2; the
 // back-solved chunk is written into the tile just consumed and stored
 // row-coalesced.  Every lane issues every store (invalid lanes repeat a valid
-// lane's store with the same data), so the counted vmcnt is exact.
+// lane's store with the same data), so the counted vmcnt is exact.  (Three
+// waves per CU fit the 2 x 25.6 KB of LDS; a one-tile variant with the next
+// chunk staged in registers ran all four SIMDs but measured 2-9 % slower on
+// the MI355X, profiles/r3i/ab_mass.txt.)
 // Requires len even and 16-B aligned src / dst (host-checked).
 template <int P>
 __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, double *dst, int len, int64_t n_lines,

@@ -5,7 +5,7 @@ entry points of include/gdm_hip.h.
 
   CutAdvection         StiffnessMatrixOperator::compute_rhs
                        (advection/stiffness.h:196-606) = uncut fused stencil
-                       of the box + host-assembled cut correction + inflow
+                       of the box (cut rows zeroed) + host-assembled cut rows + inflow
                        data, and the mass solve (mass.h:47-243 +
                        problem.h:236-267) as an exact banded solve
   CutAdvectionProblem  AdvectionProblem::run (problem.h:31-102): DiscreteTime,

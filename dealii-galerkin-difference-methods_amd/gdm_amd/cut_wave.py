@@ -1,0 +1,270 @@
+"""The cut-cell wave / heat application on the device: the
+reference's applications/wave at dim = 1 -- a GDM line cut by the FE_Q(k)
+interpolant of a level set, location "inside", no domain Dirichlet data --
+through the C ABI "Cut-cell wave" entry points of include/gdm_hip.h.
+
+  CutWave            StiffnessMatrixOperator::compute_rhs
+                     (wave/stiffness.h:42-407) = uncut 1D wave stencil of
+                     the box (cut rows zeroed) + host-assembled cut rows
+                     (surface Nitsche, ghost penalty) + (v, f) + Nitsche data;
+                     MassMatrixOperator (wave/mass.h:47-249) and the exact
+                     mass / (M + dt K) solves (wave/problem.h:457-502)
+  CutWaveProblem     WaveProblem::run (wave/problem.h:39-346): wave-rk,
+                     heat-rk (RK_CLASSIC_FOURTH_ORDER + DiscreteTime, the
+                     stages device-resident) and heat-impl (backward Euler
+                     u <- (M + dt K)^-1 (M u + dt F(t + dt))), with the
+                     postprocess table (counter, t, L2, L1, Linf) of
+                     problem.h:504-590
+  preset(name)       wave-app.cc:62-285 at dim = 1 ("wave", "heat-rk",
+                     "heat-impl")
+
+f(x, t), g(x, t) and the exact solution are the caller's functions (the
+reference's Function::value calls), evaluated on the host at the quadrature
+and surface points and uploaded, as CutAdvectionProblem does for its
+boundary data.  Every operator runs in libgdm_hip.so; there is no CPU path.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _capi
+from ._capi import GdmError, check
+from .problem import RK4_A, RK4_B, RK4_C, DiscreteTime
+
+
+def _ptr(t):
+    import torch
+
+    if not t.is_cuda or t.dtype != torch.float64 or not t.is_contiguous():
+        raise GdmError("contiguous device fp64 tensor expected")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def gauss_lobatto(n):
+    """QGaussLobatto(n) on [0, 1]: the FE_Q(n - 1) support points of a cell"""
+    if n == 2:
+        return np.array([0.0, 1.0])
+    c = np.zeros(n)
+    c[-1] = 1.0
+    r = np.polynomial.legendre.legroots(np.polynomial.legendre.legder(c))
+    return np.concatenate([[0.0], np.sort((r + 1.0) / 2.0), [1.0]])
+
+
+class CutWave:
+    """Device operators of the 1D cut wave / heat problem on [left, right].
+
+    level_set: callable phi(x) (vectorised); its FE_Q(ls_degree) interpolant
+    (values at each cell's Gauss-Lobatto points) defines inside (< 0)."""
+
+    def __init__(self, fe_degree, n_subdivisions, left, right, level_set, ls_degree=None, ghost_parameter_M=0.5,
+                 ghost_parameter_A=0.5, nitsche=None, device=0):
+        self._lib = _capi.load()
+        self._h = ctypes.c_void_p()
+        k = fe_degree if ls_degree is None else ls_degree
+        self.h = (right - left) / n_subdivisions
+        gl = gauss_lobatto(k + 1)
+        x = (left + np.arange(n_subdivisions) * self.h)[:, None] + gl[None, :] * self.h
+        ls = np.ascontiguousarray(np.asarray(level_set(x.reshape(-1)), dtype=np.float64))
+        gamma_D = 5.0 * fe_degree if nitsche is None else nitsche
+        check(self._lib.gdm_cut_wave_create(int(fe_degree), int(n_subdivisions), float(left), float(right), int(k),
+                                            ls.ctypes.data_as(ctypes.c_void_p), float(ghost_parameter_M),
+                                            float(ghost_parameter_A), float(gamma_D), int(device),
+                                            ctypes.byref(self._h)), "gdm_cut_wave_create")
+        nd, nq, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        cells = (ctypes.c_int64 * 3)()
+        check(self._lib.gdm_cut_wave_info(self._h, ctypes.byref(nd), ctypes.byref(nq), ctypes.byref(ns), cells),
+              "gdm_cut_wave_info")
+        self.n_dofs, self.n_quad, self.n_surface = nd.value, nq.value, ns.value
+        self.cells = dict(inside=cells[0], intersected=cells[1], outside=cells[2])
+        self.qx, self.qw = np.zeros(max(self.n_quad, 1)), np.zeros(max(self.n_quad, 1))
+        self.sx, self.sn = np.zeros(max(self.n_surface, 1)), np.zeros(max(self.n_surface, 1))
+        check(self._lib.gdm_cut_wave_points(self._h, *[a.ctypes.data_as(ctypes.c_void_p)
+                                                        for a in (self.qx, self.qw, self.sx, self.sn)]),
+              "gdm_cut_wave_points")
+        self.qx, self.qw = self.qx[:self.n_quad], self.qw[:self.n_quad]
+        self.sx, self.sn = self.sx[:self.n_surface], self.sn[:self.n_surface]
+        op = ctypes.c_void_p()
+        check(self._lib.gdm_cut_wave_op(self._h, ctypes.byref(op)), "gdm_cut_wave_op")
+        self._op = op
+        self.device = device
+        self.vertices = left + np.arange(n_subdivisions + 1) * self.h
+        import torch
+
+        s = torch.cuda.current_stream(device).cuda_stream
+        check(self._lib.gdm_op_set_stream(self._op, ctypes.c_void_p(s)), "gdm_op_set_stream")
+
+    def close(self):
+        if self._h:
+            self._lib.gdm_cut_wave_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def new_vector(self, n=None):
+        import torch
+
+        return torch.zeros(self.n_dofs if n is None else n, dtype=torch.float64, device="cuda:%d" % self.device)
+
+    def compute_rhs(self, u, fq, gs, out):
+        """out = [u given] (-(v', u') + Nitsche + ghost penalty) + (v, f) + Nitsche data g"""
+        check(self._lib.gdm_cut_wave_compute_rhs(self._h, _ptr(u) if u is not None else None,
+                                                 _ptr(fq) if fq is not None and self.n_quad else None,
+                                                 _ptr(gs) if gs is not None and self.n_surface else None, _ptr(out)),
+              "gdm_cut_wave_compute_rhs")
+        return out
+
+    def mass_apply(self, u, out):
+        check(self._lib.gdm_cut_wave_mass_apply(self._h, _ptr(u), _ptr(out)), "gdm_cut_wave_mass_apply")
+        return out
+
+    def mass_solve(self, rhs, x):
+        check(self._lib.gdm_cut_wave_mass_solve(self._h, _ptr(rhs), _ptr(x)), "gdm_cut_wave_mass_solve")
+        return x
+
+    def system_solve(self, dt, rhs, x):
+        check(self._lib.gdm_cut_wave_system_solve(self._h, float(dt), _ptr(rhs), _ptr(x)),
+              "gdm_cut_wave_system_solve")
+        return x
+
+    def eval_quadrature(self, u, vals):
+        check(self._lib.gdm_cut_wave_eval(self._h, _ptr(u), _ptr(vals)), "gdm_cut_wave_eval")
+        return vals
+
+    def rk_update(self, beta, k, acc_in, acc_out, alpha=0.0, y=None, Y=None):
+        check(self._lib.gdm_vec_rk_update(self._op, k.numel(), float(beta), _ptr(k), _ptr(acc_in), _ptr(acc_out),
+                                          float(alpha), _ptr(y) if Y is not None else None,
+                                          _ptr(Y) if Y is not None else None), "gdm_vec_rk_update")
+
+    def synchronize(self):
+        check(self._lib.gdm_synchronize(self._op), "gdm_synchronize")
+
+
+def preset(name):
+    """wave-app.cc parameter sets at dim = 1 (wave-app.cc:62-150 heat, :222-285
+    wave): FE degree 3, 40 cells on [-1.21, 1.21], SignedDistance::Sphere of
+    radius 1 in FE_Q(3), gamma_D = 5 p."""
+    sphere = lambda x: np.abs(x) - 1.0  # noqa: E731
+    if name == "wave":
+        k = 1.5 * math.pi
+        ex = lambda x, t: np.cos(k * np.abs(x)) * math.cos(k * t)  # noqa: E731
+        return dict(simulation=name, p=3, n=40, left=-1.21, right=1.21, level_set=sphere,
+                    gamma_M=0.25 * math.sqrt(3.0), gamma_A=0.5 * math.sqrt(3.0), nitsche=15.0, f=None, g=ex,
+                    exact=ex, start_t=0.0, end_t=2.0, cfl=0.3, cfl_pow=1.0)
+    if name in ("heat-rk", "heat-impl"):
+        ex = lambda x, t: x ** 9 * math.exp(-t)  # noqa: E731
+        f = lambda x, t: -x ** 7 * math.exp(-t) * (x * x + 72)  # noqa: E731
+        cfl, cfl_pow = (0.3 / 9.0, 2.0) if name == "heat-rk" else (0.3, 1.0)
+        return dict(simulation=name, p=3, n=40, left=-1.21, right=1.21, level_set=sphere, gamma_M=0.75,
+                    gamma_A=1.5, nitsche=15.0, f=f, g=ex, exact=ex, start_t=0.0, end_t=0.1, cfl=cfl,
+                    cfl_pow=cfl_pow)
+    raise GdmError("cut_wave.preset: %r (1D presets: wave, heat-rk, heat-impl)" % (name,))
+
+
+class CutWaveProblem:
+    """WaveProblem::run (wave/problem.h:39-346) on the device for one of the
+    1D simulation types "wave" (wave-rk), "heat-rk", "heat-impl"."""
+
+    def __init__(self, params, device=0):
+        import torch
+
+        P = dict(params)
+        self.P = P
+        self.cw = CutWave(P["p"], P["n"], P["left"], P["right"], P["level_set"], ghost_parameter_M=P["gamma_M"],
+                          ghost_parameter_A=P["gamma_A"], nitsche=P["nitsche"], device=device)
+        cw = self.cw
+        self.sim = P["simulation"]
+        self._torch = torch
+        self.u = cw.new_vector()
+        self.v = cw.new_vector() if self.sim == "wave" else None
+        self._fq = cw.new_vector(max(cw.n_quad, 1))
+        self._gs = cw.new_vector(max(cw.n_surface, 1))
+        self._vals = cw.new_vector(max(cw.n_quad, 1))
+        n_blocks = 2 if self.sim == "wave" else 1
+        self._acc = [cw.new_vector() for _ in range(n_blocks)]
+        self._Y = [cw.new_vector() for _ in range(n_blocks)]
+        self._k = [cw.new_vector() for _ in range(n_blocks)]
+        self._r = cw.new_vector()
+
+    def _upload(self, values, dst):
+        dst[:len(values)].copy_(self._torch.from_numpy(np.ascontiguousarray(values, dtype=np.float64)))
+
+    def _data(self, t):
+        """f at the quadrature points, g at the surface points (NULL when absent)"""
+        P, cw = self.P, self.cw
+        fq = gs = None
+        if P["f"] is not None and cw.n_quad:
+            self._upload(P["f"](cw.qx, t), self._fq)
+            fq = self._fq
+        if P["g"] is not None and cw.n_surface:
+            self._upload(P["g"](cw.sx, t), self._gs)
+            gs = self._gs
+        return fq, gs
+
+    def rhs(self, t, U, out):
+        """M^-1 compute_rhs(U, t) (problem.h:313-317 / heat-rk)"""
+        fq, gs = self._data(t)
+        self.cw.compute_rhs(U, fq, gs, out)
+        self.cw.mass_solve(out, out)
+        return out
+
+    def postprocess(self, t):
+        """(L2, L1, Linf) of u_h - u(t) over the inside quadrature (problem.h:504-590)"""
+        cw = self.cw
+        cw.eval_quadrature(self.u, self._vals)
+        e = self._vals[:cw.n_quad].cpu().numpy() - self.P["exact"](cw.qx, t)
+        return (math.sqrt(float(np.sum(e * e * cw.qw))), float(np.sum(np.abs(e) * cw.qw)),
+                float(np.max(np.abs(e))) if len(e) else 0.0)
+
+    def step(self, t, h):
+        cw = self.cw
+        if self.sim == "heat-impl":
+            # u <- (M + h K)^-1 (M u + h F(t + h)): F = the data part of compute_rhs
+            fq, gs = self._data(t + h)
+            cw.compute_rhs(None, fq, gs, self._r)
+            cw.mass_apply(self.u, self._k[0])
+            self._k[0].add_(self._r, alpha=h)
+            cw.system_solve(h, self._k[0], self.u)
+            return
+        y = (self.u, self.v) if self.sim == "wave" else (self.u,)
+        acc, Y, k = self._acc, self._Y, self._k
+        stage = y
+        for s in range(4):
+            ts = t + RK4_C[s] * h
+            if self.sim == "wave":
+                # k = (stage_v, M^-1 compute_rhs(stage_u)); the u block's k is stage_v itself
+                self.rhs(ts, stage[0], k[1])
+                ks = (stage[1], k[1])
+            else:
+                self.rhs(ts, stage[0], k[0])
+                ks = (k[0],)
+            last = s == 3
+            a_next = 0.0 if last else h * RK4_A[s]
+            # u block first: it reads stage_v before the v block overwrites Y_v
+            for b in range(len(y)):
+                cw.rk_update(h * RK4_B[s], ks[b], (y if s == 0 else acc)[b], (y if last else acc)[b], a_next,
+                             None if last else y[b], None if last else Y[b])
+            stage = Y
+
+    def run(self, max_steps=None):
+        """the whole time loop; returns the postprocess table [(counter, t, L2, L1, Linf)]"""
+        P, cw = self.P, self.cw
+        self._upload(P["exact"](cw.vertices, P["start_t"]), self.u)  # GDM::VectorTools::interpolate
+        if self.v is not None:
+            self.v.zero_()
+        dt = P["cfl"] * cw.h ** P["cfl_pow"]
+        time = DiscreteTime(P["start_t"], P["end_t"], dt)
+        rows = [(0, 0.0) + self.postprocess(P["start_t"])]
+        n = 0
+        while not time.is_at_end() and (max_steps is None or n < max_steps):
+            t0, h = time.t, time.next_step_size()
+            self.step(t0, h)
+            n += 1
+            rows.append((n, t0 + h) + self.postprocess(t0 + h))
+            time.advance()
+        cw.synchronize()
+        return rows

@@ -91,6 +91,7 @@ def test_device_run_reproduces_test_01_row(row):
         e = math.floor(math.log10(abs(w)))
         # beyond the printed digits: the spread of exact mass solves of the
         # cut system (cond 1e12 at p = 5: LU, banded Cholesky and CG to 1e-14
-        # move the surface Linf by up to 2e-12; test_cut_advection_golden.py)
+        # move the surface Linf by up to 2e-12; test_cut_advection_golden.py,
+        # test_cut_advection_host.py)
         slack = 5e-13 if p == 3 else 3e-12
         assert abs(g - w) <= 0.5 * 10.0 ** (e - 4) * (1 + 1e-9) + slack, (GOLD["columns"][5 + c], g, w)

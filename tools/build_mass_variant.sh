@@ -9,4 +9,4 @@ O=/root/repo/dealii-galerkin-difference-methods_amd/lib/variants/$NAME
 mkdir -p $O
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -Wno-unused-function "$@" -c $C/${GDM_MASS_SRC:-gdm_mass.hip} -o $O/mass.o &&
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libgdm_hip.so $B/gdm_capi.o $B/gdm_kernels.o $B/gdm_setup.o \
-  $B/gdm_csr.o $O/mass.o $B/gdm_rk.o $B/gdm_post.o $B/gdm_cut.o && echo "built $O"
+  $B/gdm_csr.o $O/mass.o $B/gdm_rk.o $B/gdm_post.o $B/gdm_cut.o $B/gdm_cut_advection.o $B/gdm_cut_wave.o $B/gdm_band.o && echo "built $O"
