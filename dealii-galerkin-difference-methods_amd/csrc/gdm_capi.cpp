@@ -114,7 +114,7 @@ struct gdm_op {
   // step 1 run on side_stream, filling the tail of the interior launch
   hipStream_t side_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  bool concurrent = true;  // GDM_SERIAL=1: everything on one stream
+  bool concurrent = true;  // fork / join of the z-wall launch and face step 1 on the side stream
   gdm_mesh_desc mesh{};
   int kind = 0, p = 1, dim = 1;
   int N[3] = {1, 1, 1};        // vertices per reference direction
@@ -136,9 +136,6 @@ struct gdm_op {
   double dint = 0, m_dint = 0;  // interior z scales of D (operator, mass)
   double zd8[19] = {0}, m_zd8[19] = {0};  // dint * dhat[2p - k] (operator, mass)
   int xcd_map = 1;
-  int stencil_version = 8;
-  int mass_version = 3;   // GDM_MASS=1: v1 in-place one-thread-per-line sweeps, 2: v2 two-sweep lines
-  int mass_max_wgs = 0;   // GDM_MASS_WGS: cap on the line-solve grid (0 = all lines)
   // the same for the mass operator of an advection/wave op (gdm_mass_apply)
   double *m_corrX = nullptr, *m_zt = nullptr;
   double *lrow[3] = {nullptr, nullptr, nullptr}, *invd[3] = {nullptr, nullptr, nullptr};
@@ -160,6 +157,8 @@ struct gdm_op {
   double *cg_r = nullptr, *cg_p = nullptr, *cg_Ap = nullptr, *cg_z = nullptr, *cg_invdiag = nullptr;
   std::vector<Face> faces;
   double *face_tmp = nullptr;
+  double *mass_tmp = nullptr;  // ping-pong vector of the segmented mass passes (small meshes)
+  int64_t mass_tmp_size = 0;
   int64_t face_tmp_size = 0;
   double *dot_partial = nullptr, *dot_out = nullptr;
   int n_dot_partial = 1024;
@@ -706,7 +705,7 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
   // v8 needs every x and y tile to touch at most one wall; smaller meshes use v7
   int ty8 = 32, wgs8 = 1;
   gdmk_stencil8_geom(op->p, &ty8, &wgs8);
-  const bool v8 = op->stencil_version == 8 && op->K[1] >= ty8 + 2 * op->p + 2 && op->K[0] >= 64 + 2 * op->p + 2;
+  const bool v8 = op->K[1] >= ty8 + 2 * op->p + 2 && op->K[0] >= 64 + 2 * op->p + 2;
   if (v8) a.yT1 = op->yT1d;
   a.xcd_map = op->xcd_map;
   if (as_mass) {
@@ -747,13 +746,13 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
   // table kernel, both ranges of it in one launch.
   const int p = op->p, zlo = 3 * p + 1, zhi = a.Nz - 3 * p - 1;
   const int i0 = std::max(zb, zlo), i1 = std::min(ze, zhi);
-  const bool split = a.z_toep && i1 - i0 >= 2 * p + 1 && !std::getenv("GDM_NO_ZINT");
+  const bool split = a.z_toep && i1 - i0 >= 2 * p + 1;
   const int ty = ty8, wgs = wgs8;
   const int64_t tiles = (int64_t)((a.Nx + 63) / 64) * ((a.out_y1 - a.out_y0 + ty - 1) / ty);
-  const char *rounds_env = std::getenv("GDM_ROUNDS");
-  const int rounds = rounds_env ? std::max(1, std::atoi(rounds_env)) : 1;
-  auto zchunk_for = [&](int len) {  // about `rounds` rounds of workgroups on 256 CUs
-    const int64_t chunks = std::max<int64_t>(1, (256 * wgs * rounds + tiles - 1) / tiles);
+  // one round of workgroups on 256 CUs (two rounds measured 0.93 vs 0.85 ms
+  // at C3, 0.27 vs 0.22 ms at C4: profiles/r3g/variants.txt)
+  auto zchunk_for = [&](int len) {
+    const int64_t chunks = std::max<int64_t>(1, (256 * wgs + tiles - 1) / tiles);
     return (int)std::max<int64_t>(std::min(len, 8), (len + chunks - 1) / chunks);
   };
   if (!split) {
@@ -782,7 +781,6 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
 void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
                           hipStream_t st = nullptr) {
   if (op->kind != GDM_OP_ADVECTION) return;
-  gdmk::Face2Set s2{};
   for (const Face &F : op->faces) {
     if (F.scale == 0.0) continue;
     gdmk::FaceArgs fa{};
@@ -813,32 +811,16 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     fa.stride0 = F.t0.stride;
     fa.stride1 = F.t1.stride;
     fa.scale = F.scale;
-    fa.phase = 1;  // step 1 only: step 2 of all faces is one launch below
-    if (phase != 2) hip_check(gdmk_launch_face(fa, phase == 1 && st ? st : op->stream), "face launch");
-    if (phase != 1 && fa.i0_end > fa.i0_begin && fa.i1_end > fa.i1_begin && fa.Q1 > 0) {
-      gdmk::Face2 &g = s2.f[s2.nf++];
-      g.T = fa.T;
-      g.qs1 = fa.qs1;
-      g.qc1 = fa.qc1;
-      g.w1 = fa.w1;
-      g.n0 = fa.i0_end - fa.i0_begin;
-      g.i1_begin = fa.i1_begin;
-      g.i1_end = fa.i1_end;
-      g.wmax1 = fa.wmax1;
-      g.base = fa.base;
-      g.stride0 = fa.stride0;
-      g.stride1 = fa.stride1;
-      g.scale = fa.scale;
-    }
-  }
-  if (phase != 1 && s2.nf > 0) {
-    for (int k = 0; k < s2.nf; ++k) s2.f[k].shared_edges = s2.nf > 1;
-    hip_check(gdmk_launch_face_step2_all(s2, dst_owned, op->stream), "face step 2");
+    fa.phase = phase;
+    // one face after the other: two faces share the box-edge nodes, and a
+    // concurrent step 2 (one launch, fp64 atomics on the edges) made the
+    // edge sums order-dependent, which the bit-exact rank / communicator
+    // comparisons of tests/test_host_mpi.py catch
+    hip_check(gdmk_launch_face(fa, phase == 1 && st ? st : op->stream), "face launch");
   }
 }
 
 int choose_zchunk(const gdm_op *op) {
-  if (const char *env = std::getenv("GDM_ZCHUNK")) return std::max(1, std::atoi(env));
   const int nz = op->part_axis == 2 ? (op->layout.owned_plane_end - op->layout.owned_plane_begin) : 1;
   const int ty = gdmk_stencil_tile_rows(op->p);
   const int64_t tiles = (int64_t)((op->K[0] + 63) / 64) * ((op->K[1] + ty - 1) / ty);
@@ -1070,38 +1052,70 @@ void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
   }
   const int64_t X = K[0], Y = K[1], Z = K[2];
   // v3 (gdm_mass.hip, single sweep per direction) where supported, else v2
-  // (two sweeps); the first pass reads rhs and writes x, later passes in place
-  const double *in = rhs_owned;
-  const int wg = op->mass_max_wgs;
-  const bool v3 = op->mass_version >= 3 && gdmk_mass3_chunk(op->p) > 0;
-  // timing experiment only (wrong results near the line ends): interior rows everywhere
-  static const bool notab = std::getenv("GDM_MASS_NOTAB") != nullptr;
-  auto pass = [&](int ax, int dir_kind, int64_t len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,
-                  const char *what) {
-    const LineTables &t = tab[ax];
-    const bool aligned = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(x_owned)) & 15) == 0;
+  // (two sweeps).  Large meshes: the first pass reads rhs and writes x, later
+  // passes in place.  A pass with fewer than 512 waves of lines (2D C2: 16)
+  // splits its lines into segments, which read their neighbours' input:
+  // then every pass runs out of place through the scratch vector (ping-pong
+  // ending in x)
+  const bool v3 = gdmk_mass3_chunk(op->p) > 0;
+  struct Pass {
+    int ax, dir_kind;
+    int64_t len, stride, n_lines, A, B;
+    const char *what;
+  };
+  std::vector<Pass> passes;
+  const bool part_z = part && op->part_axis == 2, part_y = part && op->part_axis == 1;
+  if (Z > 1 || part_z) passes.push_back({2, 1, Z, X * Y, X * Y, X * Y, 0, "mass z"});  // base = l, step X*Y
+  if (Y > 1 || part_y) passes.push_back({1, 1, Y, X, X * Z, X, X * Y, "mass y"});      // base = z*X*Y + x, step X
+  if (X > 1) passes.push_back({0, 0, X, 1, Y * Z, 1, 0, "mass x"});                   // contiguous rows of length X
+  auto use_v3 = [&](const Pass &q, const double *src, const double *dst) {
+    const LineTables &t = tab[q.ax];
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
     // the v3 strided kernel addresses a wave's 64 lines through one buffer
     // resource (num_records 0x7fffffff) with 32-bit position offsets: the
     // line span (len - 1) * stride plus the 64 lanes must stay below 2^31
     // bytes (3D meshes up to 645 vertices per direction), else the v2 kernel
     // (64-bit addresses) runs
-    const bool span_ok = dir_kind != 1 || ((len - 1) * stride + 64) * 8 < (int64_t)0x7fffffff;
-    if (v3 && t.l3 && span_ok && (dir_kind == 1 || (len % 2 == 0 && aligned)))
-      hip_check(gdmk_launch_mass3(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, t.l3, t.u3, t.d3,
-                                  t.cst.data(), notab ? 0 : t.row_lo, notab ? (1 << 29) : t.row_hi, op->stream),
-                what);
-    else
-      hip_check(gdmk_launch_mass_lines(op->p, dir_kind, in, x_owned, (int)len, stride, n_lines, A, B, t.lrow, t.invd,
-                                       wg, op->stream),
-                what);
-    in = x_owned;
+    const bool span_ok = q.dir_kind != 1 || ((q.len - 1) * q.stride + 64) * 8 < (int64_t)0x7fffffff;
+    return v3 && t.l3 && span_ok && (q.dir_kind == 1 || (q.len % 2 == 0 && aligned));
   };
-  const bool part_z = part && op->part_axis == 2, part_y = part && op->part_axis == 1;
-  if (Z > 1 || part_z) pass(2, 1, Z, X * Y, X * Y, X * Y, 0, "mass z");   // z lines: (x, y) -> base = l, step X*Y
-  if (Y > 1 || part_y) pass(1, 1, Y, X, X * Z, X, X * Y, "mass y");       // y lines: (x, z) -> base = z*X*Y + x, step X
-  if (X > 1) pass(0, 0, X, 1, Y * Z, 1, 0, "mass x");                     // x lines: contiguous rows of length X
+  bool segmented = false;
+  for (const Pass &q : passes) segmented = segmented || (v3 && tab[q.ax].l3 && (q.n_lines + 63) / 64 < 512);
+  double *tmp = nullptr;
+  if (segmented) {
+    if (op->mass_tmp_size < n) {  // once per operator (n is the owned size), freed with it
+      hip_check(hipMalloc(&op->mass_tmp, sizeof(double) * n), "hipMalloc");
+      keep(op, op->mass_tmp);
+      op->mass_tmp_size = n;
+    }
+    tmp = op->mass_tmp;
+  }
+  const double *in = rhs_owned;
+  const int np = (int)passes.size();
+  for (int i = 0; i < np; ++i) {
+    const Pass &q = passes[(size_t)i];
+    double *out = x_owned;
+    if (segmented) {
+      out = (np - 1 - i) % 2 == 0 ? x_owned : tmp;
+      if (out == in) {  // rhs aliases the first pass's output: move it aside
+        double *other = out == x_owned ? tmp : x_owned;
+        hip_check(hipMemcpyAsync(other, in, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+        in = other;
+      }
+    }
+    const LineTables &t = tab[q.ax];
+    if (use_v3(q, in, out))
+      hip_check(gdmk_launch_mass3(op->p, q.dir_kind, in, out, (int)q.len, q.stride, q.n_lines, q.A, q.B, t.l3, t.u3,
+                                  t.d3, t.cst.data(), t.row_lo, t.row_hi, segmented ? 1 : 0, op->stream),
+                q.what);
+    else
+      hip_check(gdmk_launch_mass_lines(op->p, q.dir_kind, in, out, (int)q.len, q.stride, q.n_lines, q.A, q.B, t.lrow,
+                                       t.invd, 0, op->stream),
+                q.what);
+    in = out;
+  }
   if (in != x_owned)
-    hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+    hip_check(hipMemcpyAsync(x_owned, in, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
 }
 
 }  // namespace
@@ -1180,15 +1194,10 @@ int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int
   hip_check(hipStreamCreateWithFlags(&op->side_stream, hipStreamNonBlocking), "hipStreamCreate");
   hip_check(hipEventCreateWithFlags(&op->ev_fork, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&op->ev_join, hipEventDisableTiming), "hipEventCreate");
-  if (const char *env = std::getenv("GDM_SERIAL")) op->concurrent = std::atoi(env) == 0;
   build_layout(op);
   build_tables(op);
   build_faces(op);
   op->zchunk = choose_zchunk(op);
-  if (const char *env = std::getenv("GDM_STENCIL")) op->stencil_version = std::atoi(env) == 7 ? 7 : 8;
-  if (const char *env = std::getenv("GDM_XCD")) op->xcd_map = std::atoi(env) != 0;
-  if (const char *env = std::getenv("GDM_MASS")) op->mass_version = std::max(1, std::min(3, std::atoi(env)));
-  if (const char *env = std::getenv("GDM_MASS_WGS")) op->mass_max_wgs = std::max(0, std::atoi(env));
   hip_check(hipMalloc(&op->dot_partial, sizeof(double) * op->n_dot_partial), "hipMalloc");
   keep(op, op->dot_partial);
   hip_check(hipMalloc(&op->dot_out, sizeof(double)), "hipMalloc");
@@ -1422,23 +1431,6 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
   if (!rhs_owned || !x_owned) return fail(GDM_ERR_ARG, "NULL vector");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
-  const int64_t n = op->layout.n_owned;
-  const int64_t X = op->K[0], Y = op->K[1], Z = op->K[2];
-  if (op->mass_version == 1) {
-    // v1: in-place sweeps, one thread per line (kept for A/B timing)
-    if (x_owned != rhs_owned)
-      hip_check(hipMemcpyAsync(x_owned, rhs_owned, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
-    if (Z > 1)
-      hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)Z, X * Y, X * Y, X * Y, 0, 1, op->lrow[2], op->invd[2],
-                                       op->stream), "chol z");
-    if (Y > 1)
-      hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)Y, X, X * Z, X, X * Y, 1, op->lrow[1], op->invd[1],
-                                       op->stream), "chol y");
-    if (X > 1)
-      hip_check(gdmk_launch_chol_lines(op->p, x_owned, (int)X, 1, Y * Z, Y * Z, 0, X, op->lrow[0], op->invd[0],
-                                       op->stream), "chol x");
-    return GDM_OK;
-  }
   mass_solve_passes(op, rhs_owned, x_owned, nullptr);
   return GDM_OK;
   GDM_GUARD_END

@@ -311,10 +311,6 @@ struct gdm_csr {
 namespace {
 
 int pick_lanes(int64_t n_rows, int64_t nnz) {
-  if (const char *e = std::getenv("GDM_CSR_LANES")) {
-    const int k = std::atoi(e);
-    if (k == 2 || k == 4 || k == 8 || k == 16 || k == 32 || k == 64) return k;
-  }
   const double avg = n_rows > 0 ? double(nnz) / double(n_rows) : 0.0;
   if (avg < 6) return 4;
   if (avg < 12) return 8;
@@ -487,9 +483,8 @@ int create_impl(int device, int64_t n_rows, int64_t n_cols, int64_t nnz, const i
                 "copy row blocks");
       // the row-block kernel everywhere (measured on config 5: cut matrix with
       // rows of 49 and 1 entries 3.11 -> 1.62 ms, full 49-entry stencil
-      // 3.97 -> 2.75 ms per SpMV); GDM_CSR_MODE=0: K lanes per row
+      // 3.97 -> 2.75 ms per SpMV)
       A->mode = 1;
-      if (const char *env = std::getenv("GDM_CSR_MODE")) A->mode = std::atoi(env) == 1 ? 1 : 0;
     }
     hip_check(hipStreamSynchronize(A->stream), "sync");
   } catch (...) {

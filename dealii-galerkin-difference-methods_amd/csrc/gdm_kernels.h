@@ -77,22 +77,7 @@ struct FaceArgs {
   int phase;  // 0: both steps, 1: step 1 only (writes T), 2: step 2 only (T -> dst)
 };
 
-constexpr int FACE_CHUNK = 256;
-
-// step 2 of one face (T -> dst), for the all-faces launch
-struct Face2 {
-  const double *T;
-  const int *qs1, *qc1;
-  const double *w1;
-  int n0, i1_begin, i1_end, wmax1;
-  int64_t base, stride0, stride1;
-  double scale;
-  int shared_edges;  // the face shares box-edge nodes with another face of the launch: atomic adds
-};
-struct Face2Set {
-  Face2 f[6];
-  int nf;
-};  // t0 nodes per workgroup of the face row kernel
+constexpr int FACE_CHUNK = 256;  // t0 nodes per workgroup of the face row kernel
 
 // hipFuncAttributeMaxDynamicSharedMemorySize is a per-device property of a
 // kernel: `mask` holds one bit per device that has it (a second thread racing
@@ -126,11 +111,14 @@ hipError_t gdmk_launch_mass_lines(int p, int dir_kind, const double *src, double
 // mass inverse v3 single-sweep line solves (gdm_mass.hip); chunk length C(p)
 // (0 = unsupported degree); tables padded with zero rows to len + 3 C + p
 int gdmk_mass3_chunk(int p);
+// allow_segments (src != dst only): lines of a pass with fewer than 512
+// waves are split into segments of >= 1 chunk with warm-ups (one more grid
+// dimension), so small meshes fill the GPU
 hipError_t gdmk_launch_mass3(int p, int dir_kind, const double *src, double *dst, int len, int64_t stride,
                              int64_t n_lines, int64_t A, int64_t B, const double *lrow, const double *urow,
-                             const double *invd, const double *cst, int row_lo, int row_hi, hipStream_t st);
+                             const double *invd, const double *cst, int row_lo, int row_hi, int allow_segments,
+                             hipStream_t st);
 hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st);
-hipError_t gdmk_launch_face_step2_all(const gdmk::Face2Set &s, double *dst, hipStream_t st);
 hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st);
 hipError_t gdmk_launch_dot(int64_t n, const double *x, const double *y, double *partial, int n_partial, double *out,
                            hipStream_t st);

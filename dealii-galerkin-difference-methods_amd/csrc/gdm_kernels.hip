@@ -51,11 +51,6 @@ namespace gdmk {
 #else
 #define GDM_DBG(a, bit) false
 #endif
-// v8 handoff: 0 = one (A, B) plane, barriers F / L per plane, 3-slot DMA
-// ring; 1 = two (A, B) planes, one barrier per plane, 2-slot DMA ring
-#ifndef GDM_STENCIL_DB
-#define GDM_STENCIL_DB 1
-#endif
 #define GDM_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
 // Coefficient tables are read-only for the whole launch and indexed by
@@ -627,15 +622,11 @@ struct Geom8 {
   // ring depth that fits that LDS share (3 slots if possible, else 2)
   static constexpr int WGS = NW <= 12 ? 2 : 1;
   static constexpr size_t LDS_CAP = (160 * 1024) / WGS;
-#if GDM_STENCIL_DB
-  // double-buffered (A, B) planes, 2-slot DMA ring
+  // double-buffered (A, B) planes, 2-slot DMA ring (the single-buffered
+  // handoff with two barriers per plane and a 3-slot ring measured slower,
+  // also at two 8-wave workgroups per CU: profiles/r2_early, r3g)
   static constexpr int NSLOT = 2;
   static constexpr int NABUF = 2;
-#else
-  static constexpr int NSLOT =
-      sizeof(double) * (size_t)(3 * USZ + ABSZ + ZTSZ + YCSZ + CORRSZ + (P + 1) * TX * NAB) <= LDS_CAP ? 3 : 2;
-  static constexpr int NABUF = 1;
-#endif
   static constexpr int YWSZ = (P + 1) * TX * NAB;  // y-wall corrections of one plane
   static constexpr int OFF_AB = NSLOT * USZ;
   static constexpr int OFF_ZT = OFF_AB + NABUF * ABSZ;
@@ -855,7 +846,6 @@ __device__ __forceinline__ void ywall8(const StencilArgs &a, const Tile7 &t) {
 template <int P, int R, int NC, int NP, int BK, int CH>
 __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) {
   using G = Geom8<P, R, NC, NP, BK>;
-#if GDM_STENCIL_DB
   // plane i: X(i) straight into (A, B) buffer i & 1 | B_i | [y walls: ywall(i) | M_i] | DMA(i + 2)
   // (the buffer was last read by the consumers' Y(i - 2), before they reached B_(i-1))
   {
@@ -906,71 +896,6 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
     }
     return;
   }
-#endif
-  constexpr int NS = G::NSLOT;
-  ldouble *u[3] = {t.u0, t.u0 + G::USZ, t.u0 + (NS > 2 ? 2 : 0) * G::USZ};
-  const int n = t.ze - t.zs;
-#pragma unroll
-  for (int k = 0; k < NS; ++k)
-    if (k < n) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + k, u[k]);
-  GDM_LDS_BARRIER();  // tables in LDS
-  dpair V1[4];
-  XWallPre<P, BK> xpre;
-  if (t.ncw > 0) xwall8_pre<P, R, NC, NP, BK>(a, t, xpre);
-  int slot = 0;
-  for (int i = 0; i < n; ++i) {
-    const int rem = n - 1 - i;  // planes issued after plane i (at most NS - 1)
-    if (GDM_DBG(a, 8))
-      ;
-    else if (NS > 2 && rem >= 2)
-      wait_dma_planes<0, 2, P, R, NC, NP, BK, CH>(t.wv);
-    else if (rem == 1)
-      wait_dma_planes<0, 1, P, R, NC, NP, BK, CH>(t.wv);
-    else
-      GDM_WAIT_VMCNT(0);
-    // the first two row groups into registers before F (overlapping the
-    // consumers' y-sweep of plane i - 1), any further ones straight into AB
-    dpair V2[4];
-    if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], t.wv, V1);
-    const bool two = G::NPASS > 1 && t.wv + NP < G::NG;
-    if (two && !GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], t.wv + NP, V2);
-    XWall<P, BK> xw0, xw1;
-    if (t.ncw > 0) {
-      xwall8_calc<P, R, NC, NP, BK>(t, u[slot], t.wv, xpre, xw0);
-      if (two) xwall8_calc<P, R, NC, NP, BK>(t, u[slot], t.wv + NP, xpre, xw1);
-    }
-    if (t.yedge && i > 0) {
-      ywall8<P, R, NC, NP, BK>(a, t);  // corrections of plane i - 1 (AB still holds it)
-      GDM_LDS_BARRIER();               // M_i-1
-    }
-    GDM_LDS_BARRIER();  // F_i
-    write_ab8<P, R, NC, NP, BK>(t, t.wv, V1);
-    if (two) write_ab8<P, R, NC, NP, BK>(t, t.wv + NP, V2);
-    if (t.ncw > 0) {
-      xwall8_add<P, BK>(t, xw0);
-      if (two) xwall8_add<P, BK>(t, xw1);
-    }
-#pragma unroll
-    for (int ps = 2; ps < G::NPASS; ++ps) {
-      const int g = t.wv + ps * NP;
-      if (g < G::NG) {
-        if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, t, u[slot], g, V1);
-        write_ab8<P, R, NC, NP, BK>(t, g, V1);
-        if (t.ncw > 0) {
-          xwall8_calc<P, R, NC, NP, BK>(t, u[slot], g, xpre, xw0);
-          xwall8_add<P, BK>(t, xw0);
-        }
-      }
-    }
-    GDM_LDS_BARRIER();  // L_i: AB(i) loaded
-    if (i + NS < n && !GDM_DBG(a, 8)) stage_plane7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + NS, u[slot]);
-    slot = slot == NS - 1 ? 0 : slot + 1;
-  }
-  if (t.yedge && n > 0) {
-    ywall8<P, R, NC, NP, BK>(a, t);
-    GDM_LDS_BARRIER();  // M_n-1
-  }
-  GDM_LDS_BARRIER();  // F_n
 }
 
 // y-sweep of the consumer's R rows from the (A, B) plane: D' and E with the
@@ -1032,12 +957,8 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
   if (zz < t.ze) {
     double D[R], E[R];
     GDM_LDS_BARRIER();  // L_i (DB: B_i)
-#if GDM_STENCIL_DB
     Tile7 tt = t;
     tt.ab0 = t.ab0 + ((zz - t.zs) & 1) * G::ABSZ;
-#else
-    const Tile7 &tt = t;
-#endif
     if (GDM_DBG(a, 1)) {
 #pragma unroll
       for (int j = 0; j < R; ++j) D[j] = E[j] = (double)zz;
@@ -1061,9 +982,6 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
         }
       }
     }
-#if !GDM_STENCIL_DB
-    GDM_LDS_BARRIER();  // F_i+1
-#endif
     if (!GDM_DBG(a, 2)) {
       if constexpr (!WALL) {
         // interior z column: out += mhat[k] E + zd[k] D with zd = dint dhat[2p - k]
@@ -1165,9 +1083,6 @@ __device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
   GDM_LDS_BARRIER();  // tables in LDS
-#if !GDM_STENCIL_DB
-  GDM_LDS_BARRIER();  // F_0
-#endif
   // ZI: the host launched this kernel only on output planes whose z columns
   // are all interior -> compile-time z bands, no table reads; otherwise every
   // plane reads its column (wall columns or the interior one) from LDS
@@ -1433,26 +1348,6 @@ __global__ void __launch_bounds__(256) face_step2_kernel(const double *__restric
   *d += scale * s;
 }
 
-// step 2 of every inflow face in one launch (blockIdx.z = face): the faces
-// run concurrently, so the box-edge nodes two faces share take both
-// contributions by hardware fp64 atomic adds (the sum of two or three terms
-// in either order)
-__global__ void __launch_bounds__(256) face_step2_all_kernel(const Face2Set s, double *__restrict__ dst) {
-  const Face2 &f = s.f[blockIdx.z];
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int i1 = f.i1_begin + (int)blockIdx.y;
-  if (t >= f.n0 || i1 >= f.i1_end) return;
-  const double *w = f.w1 + (int64_t)i1 * f.wmax1;
-  const int n = f.qc1[i1], q = f.qs1[i1];
-  double acc = 0.0;
-  for (int m = 0; m < n; ++m) acc = fma(w[m], f.T[(int64_t)(q + m) * f.n0 + t], acc);
-  double *d = dst + f.base + (int64_t)t * f.stride0 + (int64_t)(i1 - f.i1_begin) * f.stride1;
-  if (f.shared_edges)
-    unsafeAtomicAdd(d, f.scale * acc);
-  else
-    *d += f.scale * acc;
-}
-
 // ---------------------------------------------------------------------------
 // BLAS-1
 // ---------------------------------------------------------------------------
@@ -1672,7 +1567,7 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
   const int n0 = f.i0_end - f.i0_begin;
   if (n0 <= 0 || f.Q1 <= 0 || f.i1_end <= f.i1_begin) return hipSuccess;
   const size_t cell_lds = sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)f.Q0);
-  if (f.phi0 && cell_lds <= 48 * 1024 && !std::getenv("GDM_FACE_NODE")) {
+  if (f.phi0 && cell_lds <= 48 * 1024) {
     // cell form of step 1, then the usual step 2
     const int rpb = 4;
     dim3 g1c((f.Q1 + rpb - 1) / rpb);
@@ -1714,18 +1609,6 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
   if (f.phase != 1)
     hipLaunchKernelGGL(face_step2_kernel, g2, b, 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1,
                        f.dst, f.base, f.stride0, f.stride1, f.scale);
-  return hipGetLastError();
-}
-
-extern "C" hipError_t gdmk_launch_face_step2_all(const gdmk::Face2Set &s, double *dst, hipStream_t st) {
-  using namespace gdmk;
-  int gx = 0, gy = 0;
-  for (int k = 0; k < s.nf; ++k) {
-    gx = std::max(gx, (s.f[k].n0 + 255) / 256);
-    gy = std::max(gy, s.f[k].i1_end - s.f[k].i1_begin);
-  }
-  if (s.nf == 0 || gx == 0 || gy == 0) return hipSuccess;
-  hipLaunchKernelGGL(face_step2_all_kernel, dim3(gx, gy, s.nf), dim3(256), 0, st, s, dst);
   return hipGetLastError();
 }
 

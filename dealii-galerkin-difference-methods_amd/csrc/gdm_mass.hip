@@ -496,12 +496,13 @@ struct Ring3 {
 // num_records is 0x7fffffff and the position offsets are 32-bit (checked by
 // mass_solve_passes in gdm_capi.cpp, which runs the 64-bit-addressed v2
 // kernel for larger spans).  src may equal dst.
-template <int P>
+template <int P, bool SEG>
 __global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel(const double *src, double *dst, int len, int64_t stride,
                                                            int64_t n_lines, int64_t A, int64_t B,
                                                            const double *__restrict__ lrow,
                                                            const double *__restrict__ urow,
-                                                           const double *__restrict__ invd, const Cst3<P> k) {
+                                                           const double *__restrict__ invd, const Cst3<P> k,
+                                                           int seg_chunks) {
   using R = Ring3<P>;
   constexpr int C = R::C, Q = Geo3<P>::Q;
   const R r{cptr(lrow), cptr(urow), cptr(invd), k};
@@ -517,7 +518,14 @@ __global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + bw), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + bw), 0, 0x7fffffff, 0x00020000);
   const uint32_t s8 = (uint32_t)(stride * 8), last = (uint32_t)(len - 1) * s8;
-  uint32_t lo = 0, so = 0;  // byte offsets of the next load / store position
+  // segment blockIdx.y: chunks [cb, ce) of the line (seg_chunks = 0: the whole
+  // line); the march starts one chunk early at c0 = cb - 1 (a forward warm-up
+  // from a zero state, forgotten within C positions like the backward one)
+  const int n_chunks = (len + C - 1) / C;
+  const int cb = SEG ? (int)blockIdx.y * seg_chunks : 0;
+  const int ce = SEG ? min(n_chunks, cb + seg_chunks) : n_chunks;
+  const int c0 = SEG && cb > 0 ? cb - 1 : 0;
+  uint32_t lo = (uint32_t)(c0 * C) * s8, so = (uint32_t)(cb * C) * s8;  // byte offsets of the next load / store
   auto load = [&]() -> double {
     uint32_t o = min(lo, last);
     asm volatile("" : "+s"(o));
@@ -557,26 +565,43 @@ __global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel
   for (int q = 0; q < Q; ++q) fifo[q] = load();
   auto none = [](double) {};
   // the final values of chunk c - 2 are stored by the forward sweep of chunk
-  // c (fwd<.., true>), the last one or two chunks explicitly
-  r.template fwd<GDM_MASS_EDGE_MODE>(h0, h1, 0, get, none);
-  for (int c = 1;; c += 2) {
+  // c (fwd<.., true>), the last one or two chunks explicitly; the warm-up
+  // chunk's (c0 < cb) are never stored
+  if (SEG && r.fwd_const(c0 * C, c0 * C + C))
+    r.template fwd<0>(h0, h1, c0 * C, get, none);
+  else
+    r.template fwd<GDM_MASS_EDGE_MODE>(h0, h1, c0 * C, get, none);
+  for (int c = c0 + 1;; c += 2) {
+    // ---- chunk c into h1, back-solve chunk c - 1 (h0) ----
     if (c * C >= len) {
-      if (c > 1) store(h1, (c - 2) * C);
+      if (c - 2 >= cb) store(h1, (c - 2) * C);
       r.template bwd<false, GDM_MASS_EDGE_MODE>(h0, h1, (c - 1) * C);
-      store(h0, (c - 1) * C);
+      if (c - 1 >= cb) store(h0, (c - 1) * C);
       break;
     }
-    if (c == 1)
+    if (c == c0 + 1 || c - 2 < cb)
       r.step(h1, h0, c, get, none);
     else
       r.template step<true>(h1, h0, c, get, put);
-    if ((c + 1) * C >= len) {
+    if (SEG && c == ce) {  // the segment ends inside the line: chunk ce was the backward warm-up
       store(h0, (c - 1) * C);
+      break;
+    }
+    // ---- chunk c + 1 into h0, back-solve chunk c (h1) ----
+    if ((c + 1) * C >= len) {
+      if (c - 1 >= cb) store(h0, (c - 1) * C);
       r.template bwd<false, GDM_MASS_EDGE_MODE>(h1, h0, c * C);
       store(h1, c * C);
       break;
     }
-    r.template step<true>(h0, h1, c + 1, get, put);
+    if (c - 1 < cb)
+      r.step(h0, h1, c + 1, get, none);
+    else
+      r.template step<true>(h0, h1, c + 1, get, put);
+    if (SEG && c + 1 == ce) {
+      store(h1, c * C);
+      break;
+    }
   }
 }
 
@@ -591,11 +616,12 @@ __global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel
 // chunk staged in registers ran all four SIMDs but measured 2-9 % slower on
 // the MI355X, profiles/r3i/ab_mass.txt.)
 // Requires len even and 16-B aligned src / dst (host-checked).
-template <int P>
+template <int P, bool SEG>
 __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, double *dst, int len, int64_t n_lines,
                                                         const double *__restrict__ lrow,
                                                         const double *__restrict__ urow,
-                                                        const double *__restrict__ invd, const Cst3<P> k) {
+                                                        const double *__restrict__ invd, const Cst3<P> k,
+                                                        int seg_chunks) {
   using R = Ring3<P>;
   using G = Geo3<P>;
   constexpr int C = R::C, UPR = G::UPR, QL = G::QL;
@@ -662,45 +688,64 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
     GDM_FENCE();
   };
 
+  // segment blockIdx.y: chunks [cb, ce) (seg_chunks = 0: the whole line), the
+  // march from c0 = cb - 1 (forward warm-up chunk, not stored) to ce (the
+  // backward warm-up chunk when the segment ends inside the line)
+  const int n_chunks = (len + C - 1) / C;
+  const int cb = SEG ? (int)blockIdx.y * seg_chunks : 0;
+  const int ce = SEG ? min(n_chunks, cb + seg_chunks) : n_chunks;
+  const int c0 = SEG && cb > 0 ? cb - 1 : 0;
   double h0[C], h1[C];
 #pragma unroll
   for (int j = 0; j < C; ++j) h1[j] = 0.0;
-  dma(tile0, 0);
+  dma(tile0, c0 * C);
   GDM_WAIT_VMCNT(0);
-  if (C < len) dma(tile1, C);
+  if ((c0 + 1) * C < len) dma(tile1, (c0 + 1) * C);
   open_row(tile0);
   auto none = [](double) {};
-  r.template fwd<GDM_MASS_EDGE_MODE>(h0, h1, 0, get, none);
-  for (int c = 1;; c += 2) {
-    // ---- chunk c (odd): tile1, ring h1; chunk c - 1 in h0 (its input tile0 is free) ----
+  if (SEG && r.fwd_const(c0 * C, c0 * C + C))
+    r.template fwd<0>(h0, h1, c0 * C, get, none);
+  else
+    r.template fwd<GDM_MASS_EDGE_MODE>(h0, h1, c0 * C, get, none);
+  for (int c = c0 + 1;; c += 2) {
+    // ---- chunk c: tile1, ring h1; chunk c - 1 in h0 (its input tile0 is free) ----
     if (c * C >= len) {
       r.template bwd<false, GDM_MASS_EDGE_MODE>(h0, h1, (c - 1) * C);
-      write_row(tile0, h0);
-      store(tile0, (c - 1) * C);
+      if (c - 1 >= cb) {
+        write_row(tile0, h0);
+        store(tile0, (c - 1) * C);
+      }
       break;
     }
-    if (c == 1)
-      GDM_WAIT_VMCNT(0);  // only DMA(1) is in flight
+    if (c == c0 + 1 || c - 2 < cb)
+      GDM_WAIT_VMCNT(0);  // only DMA(c) is in flight (no stores were issued after it)
     else
       GDM_WAIT_VMCNT(UPR);  // DMA(c) retired; the stores issued after it may be in flight
-    if ((c + 1) * C < len) dma(tile0, (c + 1) * C);
+    if ((c + 1) * C < len && (!SEG || c + 1 <= ce)) dma(tile0, (c + 1) * C);
     open_row(tile1);
     r.step(h1, h0, c, get, none);
-    write_row(tile1, h0);
-    store(tile1, (c - 1) * C);
-    // ---- chunk c + 1 (even): tile0, ring h0; chunk c in h1 ----
+    if (c - 1 >= cb) {
+      write_row(tile1, h0);
+      store(tile1, (c - 1) * C);
+    }
+    if (SEG && c == ce) break;  // chunk ce was the backward warm-up
+    // ---- chunk c + 1: tile0, ring h0; chunk c in h1 ----
     if ((c + 1) * C >= len) {
       r.template bwd<false, GDM_MASS_EDGE_MODE>(h1, h0, c * C);
       write_row(tile1, h1);
       store(tile1, c * C);
       break;
     }
-    GDM_WAIT_VMCNT(UPR);
-    if ((c + 2) * C < len) dma(tile1, (c + 2) * C);
+    if (c - 1 < cb)
+      GDM_WAIT_VMCNT(0);
+    else
+      GDM_WAIT_VMCNT(UPR);
+    if ((c + 2) * C < len && (!SEG || c + 2 <= ce)) dma(tile1, (c + 2) * C);
     open_row(tile0);
     r.step(h0, h1, c + 1, get, none);
     write_row(tile0, h1);
     store(tile0, c * C);
+    if (SEG && c + 1 == ce) break;
   }
   GDM_WAIT_VMCNT(0);
 }
@@ -715,13 +760,9 @@ hipError_t launch_mass_lines_p(int dir_kind, const double *src, double *dst, int
   const unsigned grid = (unsigned)(max_wgs > 0 ? std::min<int64_t>(groups, max_wgs) : groups);
   const int vec = (len % 2 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(dst) & 15) == 0) ? 1 : 0;
-  // x chunk width: 16 positions (one 128-B line per row; measured 1.15 vs 1.30 ms for 8 at 512^3), GDM_MASS_XU=8
-  static const int xu = [] { const char *e = std::getenv("GDM_MASS_XU"); return e ? std::atoi(e) : 16; }();
-  if (dir_kind == 0 && xu == 16)
+  // x chunk width: 16 positions (one 128-B line per row; measured 1.15 vs 1.30 ms for 8 at 512^3)
+  if (dir_kind == 0)
     hipLaunchKernelGGL((chol_rows_kernel<P, 16>), dim3(grid), dim3(64), 0, st, src, dst, len, n_lines, vec, lrow,
-                       invd);
-  else if (dir_kind == 0)
-    hipLaunchKernelGGL((chol_rows_kernel<P, 8>), dim3(grid), dim3(64), 0, st, src, dst, len, n_lines, vec, lrow,
                        invd);
   else
     hipLaunchKernelGGL((chol_strided_kernel<P, 8>), dim3(grid), dim3(64), 0, st, src, dst, len, stride, n_lines, A,
@@ -732,7 +773,7 @@ hipError_t launch_mass_lines_p(int dir_kind, const double *src, double *dst, int
 template <int P>
 hipError_t launch_mass3_p(int dir_kind, const double *src, double *dst, int len, int64_t stride, int64_t n_lines,
                           int64_t A, int64_t B, const double *lrow, const double *urow, const double *invd,
-                          const double *cst, int row_lo, int row_hi, hipStream_t st) {
+                          const double *cst, int row_lo, int row_hi, int allow_segments, hipStream_t st) {
   Cst3<P> k;
   for (int q = 0; q < P; ++q) {
     k.l[q] = cst[q];
@@ -742,14 +783,36 @@ hipError_t launch_mass3_p(int dir_kind, const double *src, double *dst, int len,
   k.row_lo = row_lo;
   k.row_hi = row_hi;
   const unsigned grid = (unsigned)((n_lines + 63) / 64);
+  // too few lines to give every SIMD a wave (C2: 16 waves of 64 lines): split
+  // each line into segments of >= 1 chunk with forward and backward warm-ups
+  // (one wave per SIMD is the occupancy of these kernels, 1024 on the chip).
+  // Segments read their neighbours' input chunks: only out of place (src != dst)
+  constexpr int C = Geo3<P>::C;
+  const int n_chunks = (len + C - 1) / C;
+  int seg_chunks = 0, n_segs = 1;
+  if (allow_segments && src != dst && grid < 512 && n_chunks >= 4) {
+    const int want = (int)std::min<int64_t>(n_chunks, (1024 + grid - 1) / grid);
+    seg_chunks = (n_chunks + want - 1) / want;
+    n_segs = (n_chunks + seg_chunks - 1) / seg_chunks;
+    if (n_segs < 2) seg_chunks = 0, n_segs = 1;
+  }
   if (dir_kind == 0) {
     // <= 59 KB (p = 7): within the 64 KB default, no attribute needed
     constexpr size_t lds = Geo3<P>::lds_bytes();
     static_assert(lds <= 64 * 1024, "mass3_rows_kernel LDS above the default limit");
-    hipLaunchKernelGGL(mass3_rows_kernel<P>, dim3(grid), dim3(64), lds, st, src, dst, len, n_lines, lrow, urow, invd, k);
+    if (seg_chunks)
+      hipLaunchKernelGGL((mass3_rows_kernel<P, true>), dim3(grid, n_segs), dim3(64), lds, st, src, dst, len, n_lines,
+                         lrow, urow, invd, k, seg_chunks);
+    else
+      hipLaunchKernelGGL((mass3_rows_kernel<P, false>), dim3(grid), dim3(64), lds, st, src, dst, len, n_lines, lrow,
+                         urow, invd, k, 0);
   } else {
-    hipLaunchKernelGGL(mass3_strided_kernel<P>, dim3(grid), dim3(64), 0, st, src, dst, len, stride, n_lines, A, B,
-                       lrow, urow, invd, k);
+    if (seg_chunks)
+      hipLaunchKernelGGL((mass3_strided_kernel<P, true>), dim3(grid, n_segs), dim3(64), 0, st, src, dst, len, stride,
+                         n_lines, A, B, lrow, urow, invd, k, seg_chunks);
+    else
+      hipLaunchKernelGGL((mass3_strided_kernel<P, false>), dim3(grid), dim3(64), 0, st, src, dst, len, stride, n_lines,
+                         A, B, lrow, urow, invd, k, 0);
   }
   return hipGetLastError();
 }
@@ -774,13 +837,13 @@ extern "C" int gdmk_mass3_chunk(int p) {
 extern "C" hipError_t gdmk_launch_mass3(int p, int dir_kind, const double *src, double *dst, int len, int64_t stride,
                                        int64_t n_lines, int64_t A, int64_t B, const double *lrow, const double *urow,
                                        const double *invd, const double *cst, int row_lo, int row_hi,
-                                       hipStream_t st) {
+                                       int allow_segments, hipStream_t st) {
   using namespace gdmk;
   if (n_lines <= 0 || len <= 0) return hipSuccess;
   switch (p) {
-    case 3: return launch_mass3_p<3>(dir_kind, src, dst, len, stride, n_lines, A, B, lrow, urow, invd, cst, row_lo, row_hi, st);
-    case 5: return launch_mass3_p<5>(dir_kind, src, dst, len, stride, n_lines, A, B, lrow, urow, invd, cst, row_lo, row_hi, st);
-    case 7: return launch_mass3_p<7>(dir_kind, src, dst, len, stride, n_lines, A, B, lrow, urow, invd, cst, row_lo, row_hi, st);
+    case 3: return launch_mass3_p<3>(dir_kind, src, dst, len, stride, n_lines, A, B, lrow, urow, invd, cst, row_lo, row_hi, allow_segments, st);
+    case 5: return launch_mass3_p<5>(dir_kind, src, dst, len, stride, n_lines, A, B, lrow, urow, invd, cst, row_lo, row_hi, allow_segments, st);
+    case 7: return launch_mass3_p<7>(dir_kind, src, dst, len, stride, n_lines, A, B, lrow, urow, invd, cst, row_lo, row_hi, allow_segments, st);
     default: return hipErrorInvalidValue;
   }
 }

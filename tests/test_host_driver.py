@@ -210,3 +210,18 @@ def test_cut_poisson_driver_reproduces_reference_output():
     for (h, e), (hr, er), tol in zip(got, exp, (1e-2, 1.5e-4)):
         assert h == hr
         assert abs(float(e) - float(er)) / float(er) < tol, (e, er)
+
+
+DVT = os.path.join(ROOT, "dealii-galerkin-difference-methods_amd", "lib", "host", "dealii_vector_test")
+
+
+@pytest.mark.gpu
+def test_dealii_vector_adapter():
+    """gdm/hip/dealii_vector.h (EngineBlockVector, copy_owned_to/from_engine)
+    against a stand-in with deal.II's LinearAlgebra::distributed::Vector member
+    names: owned block at the engine-local owned offset on every rank of a
+    3-slab partition, round trip with ghosts zeroed, block(0) through the
+    reference <-> device point permutation, a foreign slab refused"""
+    r = subprocess.run([DVT, "0"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "dealii_vector_test ok" in r.stdout
