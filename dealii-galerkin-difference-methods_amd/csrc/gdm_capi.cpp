@@ -2192,11 +2192,11 @@ int gdm_cut_advection_destroy(gdm_cut_advection *c) {
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
-// Cut-cell wave / heat (1D; host assembly csrc/gdm_cut_wave.cpp)
+// Cut-cell wave / heat (1D and 2D; host assembly csrc/gdm_cut_wave.cpp)
 // ---------------------------------------------------------------------------
 struct gdm_cut_wave_system;
 extern "C" {
-int gdmh_cut_wave_create(int p, int n_sub, double lo, double hi, int ls_degree, const double *ls_values,
+int gdmh_cut_wave_create(int dim, int p, int n_sub, double lo, double hi, int ls_degree, const double *ls_values,
                          double gamma_M, double gamma_A, double nitsche, gdm_cut_wave_system **out, char *err,
                          size_t err_len);
 void gdmh_cut_wave_info(const gdm_cut_wave_system *S, int64_t *n_dofs, int64_t *n_quad, int64_t *n_surface,
@@ -2206,6 +2206,7 @@ void gdmh_cut_wave_csr(const gdm_cut_wave_system *S, int which, const int64_t **
 void gdmh_cut_wave_points(const gdm_cut_wave_system *S, const double **qx, const double **qw, const double **sx,
                           const double **sn, const int64_t **zero_rows, int64_t *n_zero);
 void gdmh_cut_wave_destroy(gdm_cut_wave_system *S);
+int gdmh_cut_wave_splits(const gdm_cut_wave_system *S);
 int64_t gdmh_band_cholesky(int64_t n, const int64_t *rp, const uint32_t *ci, const double *v, double alpha,
                            const int64_t *rp2, const uint32_t *ci2, const double *v2, std::vector<double> &lband);
 }
@@ -2249,17 +2250,18 @@ struct DevCsr {
 struct gdm_cut_wave {
   gdm_cut_wave_system *host = nullptr;
   gdm_op *op = nullptr;
+  int dim = 1;
   int64_t n_dofs = 0, n_quad = 0, n_surf = 0, cells[3] = {0, 0, 0};
   DevCsr C, Ff, Fg, E, M;
   int64_t *zrows = nullptr, n_zrows = 0;
-  int64_t bw_m = 0, bw_a = -1;
-  double *lband_m = nullptr, *lband_a = nullptr, dt_a = 0.0;
+  int64_t bw_m = -1, bw_a = -1, bw_k = -1;  // -1: no factor (no mass matrix when gamma_M < 0)
+  double *lband_m = nullptr, *lband_a = nullptr, *lband_k = nullptr, dt_a = 0.0;
   void release() {
     for (DevCsr *q : {&C, &Ff, &Fg, &E, &M}) q->release();
-    for (void *q : {(void *)zrows, (void *)lband_m, (void *)lband_a})
+    for (void *q : {(void *)zrows, (void *)lband_m, (void *)lband_a, (void *)lband_k})
       if (q) (void)hipFree(q);
     zrows = nullptr;
-    lband_m = lband_a = nullptr;
+    lband_m = lband_a = lband_k = nullptr;
     if (op) gdm_op_destroy(op);
     op = nullptr;
     if (host) gdmh_cut_wave_destroy(host);
@@ -2269,7 +2271,7 @@ struct gdm_cut_wave {
 
 extern "C" {
 
-int gdm_cut_wave_create(int fe_degree, int n_subdivisions, double left, double right, int ls_degree,
+int gdm_cut_wave_create(int dim, int fe_degree, int n_subdivisions, double left, double right, int ls_degree,
                         const double *ls_values, double gamma_M, double gamma_A, double nitsche, int device,
                         gdm_cut_wave **out) {
   if (!out || !ls_values) return fail(GDM_ERR_ARG, "NULL argument");
@@ -2278,20 +2280,21 @@ int gdm_cut_wave_create(int fe_degree, int n_subdivisions, double left, double r
   auto *c = new gdm_cut_wave();
   try {
     char err[256] = {0};
-    if (gdmh_cut_wave_create(fe_degree, n_subdivisions, left, right, ls_degree, ls_values, gamma_M, gamma_A, nitsche,
-                             &c->host, err, sizeof(err)) != 0) {
+    if (gdmh_cut_wave_create(dim, fe_degree, n_subdivisions, left, right, ls_degree, ls_values, gamma_M, gamma_A,
+                             nitsche, &c->host, err, sizeof(err)) != 0) {
       delete c;
       return fail(GDM_ERR_ARG, err);
     }
-    // the uncut box operator S: 1D wave -(v', u') (no box Nitsche)
+    // the uncut box operator S: wave -(grad v, grad u) of the box (no box Nitsche)
+    c->dim = dim;
     gdm_mesh_desc m{};
-    m.dim = 1;
+    m.dim = dim;
     m.fe_degree = fe_degree;
-    m.n_subdivisions[0] = n_subdivisions;
-    m.n_subdivisions[1] = m.n_subdivisions[2] = 1;
-    m.lo[0] = left;
-    m.hi[0] = right;
-    m.hi[1] = m.hi[2] = 1.0;
+    for (int d = 0; d < 3; ++d) {
+      m.n_subdivisions[d] = d < dim ? n_subdivisions : 1;
+      m.lo[d] = d < dim ? left : 0.0;
+      m.hi[d] = d < dim ? right : 1.0;
+    }
     m.n_ranks = 1;
     m.rank = 0;
     const int rc = gdm_op_create(&m, GDM_OP_WAVE, nullptr, 0, device, &c->op);
@@ -2301,6 +2304,9 @@ int gdm_cut_wave_create(int fe_degree, int n_subdivisions, double left, double r
       return rc;
     }
     gdmh_cut_wave_info(c->host, &c->n_dofs, &c->n_quad, &c->n_surf, c->cells);
+    gdm_layout L{};
+    if (gdm_op_layout(c->op, &L) != GDM_OK || L.n_local != c->n_dofs || L.n_owned != c->n_dofs)
+      throw std::runtime_error("cut wave: the box operator's layout is not the cut system's DoF range");
     hip_check(hipSetDevice(device), "hipSetDevice");
     c->C.upload(c->host, 0, c->n_dofs);
     c->Ff.upload(c->host, 1, c->n_dofs);
@@ -2314,11 +2320,13 @@ int gdm_cut_wave_create(int fe_degree, int n_subdivisions, double left, double r
     const int64_t *rp;
     const uint32_t *ci;
     const double *v;
-    gdmh_cut_wave_csr(c->host, 4, &rp, &ci, &v);
-    std::vector<double> lb;
-    c->bw_m = gdmh_band_cholesky(c->n_dofs, rp, ci, v, 0.0, nullptr, nullptr, nullptr, lb);
-    if (c->bw_m < 0) throw std::runtime_error("cut wave: mass matrix not positive definite");
-    c->lband_m = dev_upload(lb);
+    if (gamma_M >= 0.0) {
+      gdmh_cut_wave_csr(c->host, 4, &rp, &ci, &v);
+      std::vector<double> lb;
+      c->bw_m = gdmh_band_cholesky(c->n_dofs, rp, ci, v, 0.0, nullptr, nullptr, nullptr, lb);
+      if (c->bw_m < 0) throw std::runtime_error("cut wave: mass matrix not positive definite");
+      c->lband_m = dev_upload(lb);
+    }
   } catch (...) {
     c->release();
     delete c;
@@ -2344,10 +2352,10 @@ int gdm_cut_wave_points(const gdm_cut_wave *c, double *qx, double *qw, double *s
   const int64_t *zr;
   int64_t nz;
   gdmh_cut_wave_points(c->host, &hqx, &hqw, &hsx, &hsn, &zr, &nz);
-  if (qx) std::copy(hqx, hqx + c->n_quad, qx);
+  if (qx) std::copy(hqx, hqx + c->n_quad * c->dim, qx);
   if (qw) std::copy(hqw, hqw + c->n_quad, qw);
-  if (sx) std::copy(hsx, hsx + c->n_surf, sx);
-  if (sn) std::copy(hsn, hsn + c->n_surf, sn);
+  if (sx) std::copy(hsx, hsx + c->n_surf * c->dim, sx);
+  if (sn) std::copy(hsn, hsn + c->n_surf * c->dim, sn);
   return GDM_OK;
 }
 
@@ -2391,6 +2399,7 @@ int gdm_cut_wave_mass_apply(gdm_cut_wave *c, const double *u, double *out) {
 
 int gdm_cut_wave_mass_solve(gdm_cut_wave *c, const double *rhs, double *x) {
   if (!c || !rhs || !x) return fail(GDM_ERR_ARG, "NULL argument");
+  if (c->bw_m < 0) return fail(GDM_ERR_ARG, "gdm_cut_wave_mass_solve: no mass matrix (gamma_M < 0)");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(c->op->device), "hipSetDevice");
   if (x != rhs)
@@ -2424,6 +2433,28 @@ int gdm_cut_wave_system_solve(gdm_cut_wave *c, double dt, const double *rhs, dou
   if (x != rhs)
     hip_check(hipMemcpyAsync(x, rhs, sizeof(double) * c->n_dofs, hipMemcpyDeviceToDevice, c->op->stream), "copy");
   hip_check(gdmk_launch_band_solve(c->n_dofs, c->bw_a, c->lband_a, x, c->op->stream), "band solve");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_wave_stiffness_solve(gdm_cut_wave *c, const double *rhs, double *x) {
+  if (!c || !rhs || !x) return fail(GDM_ERR_ARG, "NULL argument");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  if (c->bw_k < 0) {
+    const int64_t *rp;
+    const uint32_t *ci;
+    const double *v;
+    gdmh_cut_wave_csr(c->host, 5, &rp, &ci, &v);
+    std::vector<double> lb;
+    const int64_t bw = gdmh_band_cholesky(c->n_dofs, rp, ci, v, 0.0, nullptr, nullptr, nullptr, lb);
+    if (bw < 0) throw std::runtime_error("cut wave: stiffness matrix not positive definite");
+    c->lband_k = dev_upload(lb);
+    c->bw_k = bw;
+  }
+  if (x != rhs)
+    hip_check(hipMemcpyAsync(x, rhs, sizeof(double) * c->n_dofs, hipMemcpyDeviceToDevice, c->op->stream), "copy");
+  hip_check(gdmk_launch_band_solve(c->n_dofs, c->bw_k, c->lband_k, x, c->op->stream), "band solve");
   return GDM_OK;
   GDM_GUARD_END
 }

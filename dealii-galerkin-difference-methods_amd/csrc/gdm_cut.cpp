@@ -112,6 +112,387 @@ void saye_unit(const Bilinear &f, const std::vector<double> &qx, const std::vect
   }
 }
 
+std::vector<double> gauss_lobatto(int n) {
+  // the roots of P'_{n-1} by Newton from the Chebyshev-Gauss-Lobatto guesses
+  std::vector<double> x(n);
+  x[0] = 0.0;
+  x[n - 1] = 1.0;
+  const int m = n - 1;
+  for (int i = 1; i < m; ++i) {
+    double t = -std::cos(M_PI * i / m);  // on [-1, 1]
+    for (int it = 0; it < 100; ++it) {
+      double p0 = 1.0, p1 = t;
+      for (int j = 2; j <= m; ++j) {
+        const double p2 = ((2 * j - 1) * t * p1 - (j - 1) * p0) / j;
+        p0 = p1;
+        p1 = p2;
+      }
+      const double dp = m * (t * p1 - p0) / (t * t - 1.0);                  // P'_m
+      const double d2p = (2.0 * t * dp - m * (m + 1) * p1) / (1.0 - t * t);  // P''_m
+      const double dt = dp / d2p;
+      t -= dt;
+      if (std::fabs(dt) < 1e-16) break;
+    }
+    x[i] = 0.5 * (t + 1.0);
+  }
+  std::sort(x.begin(), x.end());
+  return x;
+}
+
+namespace {
+
+// monomial coefficients A[a][i] of the 1D Lagrange polynomials through x
+void lagrange_monomials(const std::vector<double> &x, double A[10][10]) {
+  const int n = (int)x.size();
+  for (int a = 0; a < n; ++a) {
+    double c[10] = {1.0};
+    int deg = 0;
+    double den = 1.0;
+    for (int b = 0; b < n; ++b) {
+      if (b == a) continue;
+      // c *= (s - x_b)
+      for (int i = deg + 1; i >= 0; --i) c[i] = (i > 0 ? c[i - 1] : 0.0) - x[b] * c[i];
+      ++deg;
+      den *= x[a] - x[b];
+    }
+    for (int i = 0; i < n; ++i) A[a][i] = c[i] / den;
+  }
+}
+
+// inverse of a small dense matrix (Gauss-Jordan, partial pivoting)
+void invert(int n, double M[10][10], double R[10][10]) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) R[i][j] = i == j ? 1.0 : 0.0;
+  for (int c = 0; c < n; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < n; ++r)
+      if (std::fabs(M[r][c]) > std::fabs(M[piv][c])) piv = r;
+    for (int j = 0; j < n; ++j) {
+      std::swap(M[c][j], M[piv][j]);
+      std::swap(R[c][j], R[piv][j]);
+    }
+    const double d = M[c][c];
+    for (int j = 0; j < n; ++j) {
+      M[c][j] /= d;
+      R[c][j] /= d;
+    }
+    for (int r = 0; r < n; ++r) {
+      if (r == c || M[r][c] == 0.0) continue;
+      const double f = M[r][c];
+      for (int j = 0; j < n; ++j) {
+        M[r][j] -= f * M[c][j];
+        R[r][j] -= f * R[c][j];
+      }
+    }
+  }
+}
+
+void powers(int k, double x, double *p, double *d, double *d2) {
+  for (int i = 0; i <= k; ++i) {
+    p[i] = i == 0 ? 1.0 : p[i - 1] * x;
+    d[i] = i == 0 ? 0.0 : i * (i == 1 ? 1.0 : p[i - 2] * x);
+    d2[i] = i < 2 ? 0.0 : i * (i - 1) * (i == 2 ? 1.0 : p[i - 3] * x);
+  }
+}
+
+constexpr double kLimit = 1e-11;  // limit_to_be_definite, lower_bound_implicit_function
+constexpr int kMaxBoxSplits = 4, kMaxRootSplits = 2;
+constexpr double kRootTol = 1e-12;
+
+bool indefinite(double lo, double hi) { return !(lo > 0.0 || hi < 0.0); }
+double lower_abs(double lo, double hi) { return (lo > 0.0 || hi < 0.0) ? std::min(std::fabs(lo), std::fabs(hi)) : 0.0; }
+int sgn(double x) { return (x > 0.0) - (x < 0.0); }
+
+// RootFinder::find_roots of the 1D function L(x) -> (value, first, second
+// derivative) on [a, b]: a sign change at the ends gives a root (bisected to
+// machine precision); otherwise Taylor bounds at the centre and up to two
+// halvings
+template <class Line>
+void find_roots(const Line &L, double a, double b, int depth, std::vector<double> &roots) {
+  double fa, fb, d1, d2;
+  L(a, fa, d1, d2);
+  L(b, fb, d1, d2);
+  if (sgn(fa) != sgn(fb)) {
+    if (fa == 0.0) {
+      roots.push_back(a);
+      return;
+    }
+    double lo = a, hi = b, flo = fa;
+    for (int it = 0; it < 200; ++it) {
+      const double m = 0.5 * (lo + hi);
+      if (m == lo || m == hi) break;
+      double fm;
+      L(m, fm, d1, d2);
+      if (fm == 0.0) {
+        roots.push_back(m);
+        return;
+      }
+      if ((fm < 0.0) == (flo < 0.0)) {
+        lo = m;
+        flo = fm;
+      } else {
+        hi = m;
+      }
+    }
+    roots.push_back(0.5 * (lo + hi));
+    return;
+  }
+  const double c = 0.5 * (a + b), dx = 0.5 * (b - a);
+  double v;
+  L(c, v, d1, d2);
+  const double spread = std::fabs(d1) * dx + 0.5 * std::fabs(d2) * dx * dx;
+  if (!indefinite(v - spread, v + spread)) return;
+  if (depth < kMaxRootSplits) {
+    find_roots(L, a, c, depth + 1, roots);
+    find_roots(L, c, b, depth + 1, roots);
+  }
+}
+
+void unique_sorted(std::vector<double> &r) {
+  std::sort(r.begin(), r.end());
+  std::vector<double> out;
+  for (double x : r)
+    if (out.empty() || std::fabs(x - out.back()) >= kRootTol) out.push_back(x);
+  r.swap(out);
+}
+
+struct PolyGen {
+  const TensorPoly &f;
+  const std::vector<double> &qx, &qw;
+  std::vector<QPoint> &inside;
+  std::vector<SPoint> &surface;
+  int n_splits = 0;
+
+  void tensor(const double lo[2], const double hi[2]) {
+    const double L0 = hi[0] - lo[0], L1 = hi[1] - lo[1];
+    for (size_t b = 0; b < qx.size(); ++b)
+      for (size_t a = 0; a < qx.size(); ++a)
+        inside.push_back({lo[0] + L0 * qx[a], lo[1] + L1 * qx[b], qw[a] * qw[b] * L0 * L1});
+  }
+
+  void generate(const double lo[2], const double hi[2], int n_box_splits) {
+    const double c[2] = {0.5 * (lo[0] + hi[0]), 0.5 * (lo[1] + hi[1])};
+    const double dx[2] = {0.5 * (hi[0] - lo[0]), 0.5 * (hi[1] - lo[1])};
+    double val, g[2], H[2][2];
+    f.derivatives(c[0], c[1], val, g, H);
+    double spread = std::fabs(g[0]) * dx[0] + std::fabs(g[1]) * dx[1];
+    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j) spread += 0.5 * std::fabs(H[i][j]) * dx[i] * dx[j];
+    double vmin = val - spread, vmax = val + spread;
+    for (double vs : {lo[0], hi[0]})
+      for (double vt : {lo[1], hi[1]}) {
+        const double fv = f.value(vs, vt);
+        vmin = std::min(vmin, fv);
+        vmax = std::max(vmax, fv);
+      }
+    if (vmin > kLimit) return;
+    if (vmax < -kLimit) {
+      tensor(lo, hi);
+      return;
+    }
+    double low[2];
+    for (int i = 0; i < 2; ++i) {
+      const double dg = std::fabs(H[i][0]) * dx[0] + std::fabs(H[i][1]) * dx[1];
+      low[i] = lower_abs(g[i] - dg, g[i] + dg);
+    }
+    // first of equal ones (within 1e-12 relative: symmetric cells tie up to round-off)
+    const int hdir = low[1] > low[0] + 1e-12 * std::max(low[0], low[1]) ? 1 : 0;
+    if (low[hdir] > kLimit) {
+      height(hdir, lo, hi);
+    } else if (n_box_splits < kMaxBoxSplits) {
+      ++n_splits;
+      const int d = (hi[0] - lo[0]) >= (hi[1] - lo[1]) ? 0 : 1;
+      const double mid = 0.5 * (lo[d] + hi[d]);
+      double hl[2] = {hi[0], hi[1]}, lr[2] = {lo[0], lo[1]};
+      hl[d] = mid;
+      lr[d] = mid;
+      generate(lo, hl, n_box_splits + 1);
+      generate(lr, hi, n_box_splits + 1);
+    } else if (f.value(c[0], c[1]) < 0.0) {  // midpoint rule
+      inside.push_back({c[0], c[1], 4.0 * dx[0] * dx[1]});
+    }
+  }
+
+  void height(int hdir, const double lo[2], const double hi[2]) {
+    const int cdir = 1 - hdir;
+    const double c_lo = lo[cdir], c_hi = hi[cdir], h_lo = lo[hdir], h_hi = hi[hdir];
+    auto at = [&](double cc, double hh, double &s, double &t) {
+      s = cdir == 0 ? cc : hh;
+      t = cdir == 0 ? hh : cc;
+    };
+    // the level set along direction dir through the point (cc, hh) with the other coordinate fixed
+    auto line = [&](int dir, double fixed_c, double fixed_h) {
+      return [&, dir, fixed_c, fixed_h](double x, double &v, double &d1, double &d2) {
+        double s, t, g[2], H[2][2];
+        if (dir == cdir)
+          at(x, fixed_h, s, t);
+        else
+          at(fixed_c, x, s, t);
+        f.derivatives(s, t, v, g, H);
+        d1 = g[dir];
+        d2 = H[dir][dir];
+      };
+    };
+    std::vector<double> roots;
+    find_roots(line(cdir, 0.0, h_lo), c_lo, c_hi, 0, roots);
+    find_roots(line(cdir, 0.0, h_hi), c_lo, c_hi, 0, roots);
+    unique_sorted(roots);
+    std::vector<double> edges;
+    edges.push_back(c_lo);
+    edges.insert(edges.end(), roots.begin(), roots.end());
+    edges.push_back(c_hi);
+    const double Lh = h_hi - h_lo;
+    const int nq = (int)qx.size();
+    std::vector<double> hr;
+    for (size_t e = 0; e + 1 < edges.size(); ++e) {
+      const double a = edges[e], L = edges[e + 1] - a;
+      if (!(L > 0.0)) continue;
+      double s, t;
+      at(a + 0.5 * L, h_lo, s, t);
+      const double sb = f.value(s, t);
+      at(a + 0.5 * L, h_hi, s, t);
+      const double st = f.value(s, t);
+      if (sb > 0.0 && st > 0.0) continue;
+      for (int k = 0; k < nq; ++k) {
+        const double cc = a + L * qx[k], wc = qw[k] * L;
+        if (sb < 0.0 && st < 0.0) {
+          for (int m = 0; m < nq; ++m) {
+            at(cc, h_lo + Lh * qx[m], s, t);
+            inside.push_back({s, t, wc * qw[m] * Lh});
+          }
+          continue;
+        }
+        hr.clear();
+        find_roots(line(hdir, cc, 0.0), h_lo, h_hi, 0, hr);
+        unique_sorted(hr);
+        double prev = h_lo;
+        for (size_t r = 0; r <= hr.size(); ++r) {
+          const double nxt = r < hr.size() ? hr[r] : h_hi, Ls = nxt - prev;
+          if (Ls > 0.0) {
+            at(cc, prev + 0.5 * Ls, s, t);
+            if (f.value(s, t) < 0.0)
+              for (int m = 0; m < nq; ++m) {
+                at(cc, prev + Ls * qx[m], s, t);
+                inside.push_back({s, t, wc * qw[m] * Ls});
+              }
+          }
+          prev = nxt;
+        }
+        if (hr.size() == 1) {
+          double v, g[2], H[2][2];
+          at(cc, hr[0], s, t);
+          f.derivatives(s, t, v, g, H);
+          const double ng = std::hypot(g[0], g[1]);
+          surface.push_back({s, t, wc * ng / std::fabs(g[hdir]), g[0] / ng, g[1] / ng});
+        }
+      }
+    }
+  }
+};
+
+}  // namespace
+
+void TensorPoly::interpolate(int k_, const double *vals, const std::vector<double> &support) {
+  k = k_;
+  double A[10][10] = {};
+  lagrange_monomials(support, A);
+  const int n = k + 1;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double c = 0.0;
+      for (int a = 0; a < n; ++a)
+        for (int b = 0; b < n; ++b) c += A[a][i] * vals[a + n * b] * A[b][j];
+      C[i][j] = c;
+    }
+}
+
+double TensorPoly::value(double s, double t) const {
+  double r = 0.0;
+  for (int i = k; i >= 0; --i) {
+    double row = 0.0;
+    for (int j = k; j >= 0; --j) row = row * t + C[i][j];
+    r = r * s + row;
+  }
+  return r;
+}
+
+void TensorPoly::derivatives(double s, double t, double &v, double g[2], double H[2][2]) const {
+  double ps[10], ds[10], d2s[10], pt[10], dt[10], d2t[10];
+  powers(k, s, ps, ds, d2s);
+  powers(k, t, pt, dt, d2t);
+  double r[6] = {0, 0, 0, 0, 0, 0};  // v, fs, ft, fss, fst, ftt
+  for (int i = 0; i <= k; ++i) {
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0;  // sum_j C_ij t^j, d/dt, d2/dt2
+    for (int j = 0; j <= k; ++j) {
+      c0 += C[i][j] * pt[j];
+      c1 += C[i][j] * dt[j];
+      c2 += C[i][j] * d2t[j];
+    }
+    r[0] += ps[i] * c0;
+    r[1] += ds[i] * c0;
+    r[2] += ps[i] * c1;
+    r[3] += d2s[i] * c0;
+    r[4] += ds[i] * c1;
+    r[5] += ps[i] * c2;
+  }
+  v = r[0];
+  g[0] = r[1];
+  g[1] = r[2];
+  H[0][0] = r[3];
+  H[0][1] = H[1][0] = r[4];
+  H[1][1] = r[5];
+}
+
+int bernstein_location(int dim, int k, const double *vals, const std::vector<double> &support) {
+  const int n = k + 1;
+  double B[10][10], T[10][10];
+  for (int a = 0; a < n; ++a)
+    for (int i = 0; i < n; ++i) {
+      double binom = 1.0;
+      for (int q = 1; q <= i; ++q) binom = binom * (k - i + q) / q;
+      B[a][i] = binom * std::pow(support[a], i) * std::pow(1.0 - support[a], k - i);
+    }
+  invert(n, B, T);
+  double lo = INFINITY, hi = -INFINITY;
+  if (dim == 1) {
+    for (int i = 0; i < n; ++i) {
+      double c = 0.0;
+      for (int a = 0; a < n; ++a) c += T[i][a] * vals[a];
+      lo = std::min(lo, c);
+      hi = std::max(hi, c);
+    }
+  } else {
+    // T V T^T with V[a][b] = vals[a + n b]
+    double TV[10][10];
+    for (int i = 0; i < n; ++i)
+      for (int b = 0; b < n; ++b) {
+        double c = 0.0;
+        for (int a = 0; a < n; ++a) c += T[i][a] * vals[a + n * b];
+        TV[i][b] = c;
+      }
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        double c = 0.0;
+        for (int b = 0; b < n; ++b) c += TV[i][b] * T[j][b];
+        lo = std::min(lo, c);
+        hi = std::max(hi, c);
+      }
+  }
+  if (hi < 0.0) return INSIDE;
+  if (lo > 0.0) return OUTSIDE;
+  return INTERSECTED;
+}
+
+void saye_poly(const TensorPoly &f, const std::vector<double> &qx, const std::vector<double> &qw,
+               std::vector<QPoint> &inside, std::vector<SPoint> &surface, int *n_splits) {
+  inside.clear();
+  surface.clear();
+  PolyGen gen{f, qx, qw, inside, surface};
+  const double lo[2] = {0.0, 0.0}, hi[2] = {1.0, 1.0};
+  gen.generate(lo, hi, 0);
+  if (n_splits) *n_splits += gen.n_splits;
+}
+
 }  // namespace gdm
 
 struct gdm_cut_system {

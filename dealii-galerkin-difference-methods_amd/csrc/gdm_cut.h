@@ -1,6 +1,7 @@
-// gdm_cut.h -- shared host pieces of the 2D cut-cell assembly (gdm_cut.cpp:
-// cut Poisson, gdm_cut_advection.cpp: cut advection): the FE_Q(1) cell level
-// set, deal.II's QuadratureGenerator (Saye) on the unit cell, 1D shapes.
+// gdm_cut.h -- shared host pieces of the cut-cell assembly (gdm_cut.cpp:
+// cut Poisson, gdm_cut_advection.cpp: cut advection, gdm_cut_wave.cpp: cut
+// wave / heat): the FE_Q(1) and FE_Q(k) cell level sets, deal.II's
+// QuadratureGenerator (Saye) on the unit cell, 1D shapes.
 #pragma once
 
 #include <vector>
@@ -35,6 +36,31 @@ inline double linear_root(double f0, double f1) {
 // level set (reference measure; surface normal = grad f / |grad f|)
 void saye_unit(const Bilinear &f, const std::vector<double> &qx, const std::vector<double> &qw,
                std::vector<QPoint> &inside, std::vector<SPoint> &surface);
+
+// FE_Q(k) level set of one cell in reference coordinates (k <= 9):
+// f(s, t) = sum_ij C[i][j] s^i t^j, the tensor-product Lagrange interpolant
+// of the values at the cell's Gauss-Lobatto support points
+struct TensorPoly {
+  int k = 1;
+  double C[10][10] = {};
+  // vals[a + (k + 1) b] = f(x_a, x_b) on the support points x (a along s)
+  void interpolate(int k_, const double *vals, const std::vector<double> &support);
+  double value(double s, double t) const;
+  void derivatives(double s, double t, double &v, double g[2], double H[2][2]) const;
+};
+
+// Gauss-Lobatto points of n >= 2 points on [0, 1] (FE_Q support points)
+std::vector<double> gauss_lobatto(int n);
+
+// NonMatching::MeshClassifier of one cell: the Lagrange values mapped to the
+// Bernstein basis of degree k (tensor product in 2D); all < 0 INSIDE, all > 0
+// OUTSIDE, else INTERSECTED
+int bernstein_location(int dim, int k, const double *vals, const std::vector<double> &support);
+
+// QuadratureGenerator<2> (Saye) for a FE_Q(k) cell level set on the unit box,
+// with deal.II's box splits / midpoint fallback; *n_splits counts splits
+void saye_poly(const TensorPoly &f, const std::vector<double> &qx, const std::vector<double> &qw,
+               std::vector<QPoint> &inside, std::vector<SPoint> &surface, int *n_splits);
 
 struct Shapes {
   // values / reference derivatives of the p+1 1D shapes at a point

@@ -49,11 +49,11 @@
 #include "gdm_setup.h"
 
 struct gdm_cut_wave_system {
-  int p = 0, n = 0, k = 0;
+  int dim = 1, p = 0, n = 0, k = 0, n_splits = 0;
   double lo = 0.0, h = 0.0, gM = 0.0, gA = 0.0, nitsche = 0.0;
   std::vector<int8_t> loc;
-  std::vector<double> qx, qw;  // inside quadrature: global x, JxW
-  std::vector<double> sx, sn;  // surface points: global x, normal
+  std::vector<double> qx, qw;  // inside quadrature: global coordinates [n][dim], JxW
+  std::vector<double> sx, sn;  // surface points: global coordinates [n][dim], normal [n][dim]
   std::vector<int64_t> zero_rows;
   // CSR: C [N][N], Ff [N][nq], Fg [N][ns], E [nq][N], M [N][N], S [N][N]
   std::vector<int64_t> c_rp, ff_rp, fg_rp, e_rp, m_rp, s_rp;
@@ -66,62 +66,45 @@ namespace {
 
 using namespace gdm;
 
-// Gauss-Lobatto points of n >= 2 points on [0, 1] (FE_Q support points):
-// the roots of P'_{n-1} by Newton from the Chebyshev-Gauss-Lobatto guesses
-std::vector<double> gauss_lobatto(int n) {
-  std::vector<double> x(n);
-  x[0] = 0.0;
-  x[n - 1] = 1.0;
-  const int m = n - 1;
-  for (int i = 1; i < m; ++i) {
-    double t = -std::cos(M_PI * i / m);  // on [-1, 1]
-    for (int it = 0; it < 100; ++it) {
-      // P_m and its derivatives by the recurrence
-      double p0 = 1.0, p1 = t;
-      for (int j = 2; j <= m; ++j) {
-        const double p2 = ((2 * j - 1) * t * p1 - (j - 1) * p0) / j;
-        p0 = p1;
-        p1 = p2;
-      }
-      const double dp = m * (t * p1 - p0) / (t * t - 1.0);        // P'_m
-      const double d2p = (2.0 * t * dp - m * (m + 1) * p1) / (1.0 - t * t);  // P''_m
-      const double dt = dp / d2p;
-      t -= dt;
-      if (std::fabs(dt) < 1e-16) break;
-    }
-    x[i] = 0.5 * (t + 1.0);
-  }
-  std::sort(x.begin(), x.end());
-  return x;
-}
-
-// band accumulator of an N x N matrix with couplings |i - j| <= R
-struct Band1 {
-  int64_t N = 0;
-  int R = 0;
+// accumulator of an N^dim x N^dim matrix with couplings |i_d - j_d| <= R per
+// direction (DoF index = ix + N iy): one dense slot row per DoF
+struct Slots {
+  int64_t N = 0, rows = 0;
+  int dim = 1, R = 0, SW = 1, SL = 1;
   std::vector<double> v;
   std::vector<uint8_t> touched;
-  void init(int64_t N_, int R_) {
+  void init(int dim_, int64_t N_, int R_) {
+    dim = dim_;
     N = N_;
     R = R_;
-    v.assign((size_t)N * (2 * R + 1), 0.0);
+    SW = 2 * R + 1;
+    SL = dim == 1 ? SW : SW * SW;
+    rows = dim == 1 ? N : N * N;
+    v.assign((size_t)rows * SL, 0.0);
     touched.assign(v.size(), 0);
   }
+  int64_t slot(int64_t i, int64_t j) const {
+    if (dim == 1) return j - i + R;
+    return (j / N - i / N + R) * SW + (j % N - i % N + R);
+  }
   void add(int64_t i, int64_t j, double x) {
-    const size_t o = (size_t)i * (2 * R + 1) + (size_t)(j - i + R);
+    const size_t o = (size_t)i * SL + (size_t)slot(i, j);
     v[o] += x;
     touched[o] = 1;
   }
   void csr(std::vector<int64_t> &rp, std::vector<uint32_t> &ci, std::vector<double> &vals, bool unit_diag) const {
-    rp.assign((size_t)N + 1, 0);
+    rp.assign((size_t)rows + 1, 0);
     ci.clear();
     vals.clear();
-    for (int64_t i = 0; i < N; ++i) {
-      for (int k = 0; k <= 2 * R; ++k) {
-        const int64_t j = i + k - R;
-        const bool diag = k == R;
-        if (j < 0 || j >= N) continue;
-        const size_t o = (size_t)i * (2 * R + 1) + (size_t)k;
+    for (int64_t i = 0; i < rows; ++i) {
+      const int64_t ix = dim == 1 ? i : i % N, iy = dim == 1 ? 0 : i / N;
+      for (int k = 0; k < SL; ++k) {
+        const int64_t dx = (dim == 1 ? k : k % SW) - R, dy = dim == 1 ? 0 : k / SW - R;
+        const int64_t jx = ix + dx, jy = iy + dy;
+        if (jx < 0 || jx >= N || jy < 0 || (dim == 2 && jy >= N)) continue;
+        const int64_t j = dim == 1 ? jx : jy * N + jx;
+        const bool diag = j == i;
+        const size_t o = (size_t)i * SL + (size_t)k;
         if (!touched[o] && !(diag && unit_diag)) continue;
         double x = v[o];
         if (diag && unit_diag && x == 0.0) x = 1.0;
@@ -156,7 +139,7 @@ void triplets_csr(std::vector<Trip> t, int64_t rows, std::vector<int64_t> &rp, s
   for (int64_t r = 0; r < rows; ++r) rp[(size_t)r + 1] += rp[(size_t)r];
 }
 
-void assemble(gdm_cut_wave_system &S, const double *ls_values) {
+void assemble1d(gdm_cut_wave_system &S, const double *ls_values) {
   const int p = S.p, n = S.n, k = S.k, n1 = p + 1;
   const int64_t N = n + 1;
   const double h = S.h;
@@ -168,11 +151,8 @@ void assemble(gdm_cut_wave_system &S, const double *ls_values) {
   std::vector<std::vector<std::pair<double, double>>> cq(n), cs(n);
   for (int c = 0; c < n; ++c) {
     const double *vals = ls_values + (size_t)c * (k + 1);
-    bool neg = true, pos = true;
-    for (int a = 0; a <= k; ++a) {
-      neg = neg && vals[a] < 0.0;
-      pos = pos && vals[a] > 0.0;
-    }
+    const int where = bernstein_location(1, k, vals, gl);
+    const bool neg = where == INSIDE, pos = where == OUTSIDE;
     auto phi = [&](double s) {
       double r = 0.0;
       for (int a = 0; a <= k; ++a) {
@@ -238,10 +218,10 @@ void assemble(gdm_cut_wave_system &S, const double *ls_values) {
       for (int i = 0; i < n1; ++i) full_row[(size_t)(off_of(c) + i)] = 1;
   for (int64_t r = 0; r < N; ++r)
     if (full_row[(size_t)r]) S.zero_rows.push_back(r);
-  Band1 C, M, K;
-  C.init(N, p + 1);
-  M.init(N, p + 1);
-  K.init(N, p + 1);
+  Slots C, M, K;
+  C.init(1, N, p + 1);
+  M.init(1, N, p + 1);
+  K.init(1, N, p + 1);
   std::vector<Trip> ff, fg, ev;
   Shapes sh{};
   for (int c = 0; c < n; ++c) {
@@ -305,7 +285,7 @@ void assemble(gdm_cut_wave_system &S, const double *ls_values) {
       for (const auto &a : jump)
         for (const auto &b : jump) {
           C.add(a.first, b.first, -0.5 * S.gA * h * a.second * b.second);
-          M.add(a.first, b.first, 0.5 * S.gM * h * h * h * a.second * b.second);
+          if (S.gM >= 0.0) M.add(a.first, b.first, 0.5 * S.gM * h * h * h * a.second * b.second);
           K.add(a.first, b.first, 0.5 * S.gA * h * h * h * a.second * b.second);
         }
     }
@@ -318,6 +298,166 @@ void assemble(gdm_cut_wave_system &S, const double *ls_values) {
   triplets_csr(ev, (int64_t)S.qx.size(), S.e_rp, S.e_ci, S.e_v);
 }
 
+// dim = 2: cells (cx, cy) lexicographic, DoF (ix, iy) -> ix + N iy; the
+// caller's level-set values per cell at the (k+1)^2 Gauss-Lobatto points
+// (a along x fastest); quadrature by saye_poly (gdm_cut.cpp)
+void assemble2d(gdm_cut_wave_system &S, const double *ls_values) {
+  const int p = S.p, n = S.n, k = S.k, n1 = p + 1, nd = n1 * n1, nk = (k + 1) * (k + 1);
+  const int64_t N = n + 1, NN = N * N;
+  const double h = S.h;
+  std::vector<double> gx, gw;
+  gauss_unit(n1, gx, gw);
+  const std::vector<double> gl = gauss_lobatto(k + 1);
+  S.loc.assign((size_t)n * n, OUTSIDE);
+  std::vector<std::vector<QPoint>> cq((size_t)n * n);
+  std::vector<std::vector<SPoint>> cs((size_t)n * n);
+  for (int cy = 0; cy < n; ++cy)
+    for (int cx = 0; cx < n; ++cx) {
+      const size_t c = (size_t)cy * n + cx;
+      const double *vals = ls_values + c * nk;
+      S.loc[c] = (int8_t)bernstein_location(2, k, vals, gl);
+      if (S.loc[c] == INSIDE) {
+        for (int b = 0; b < n1; ++b)
+          for (int a = 0; a < n1; ++a) cq[c].push_back({gx[a], gx[b], gw[a] * gw[b]});
+      } else if (S.loc[c] == INTERSECTED) {
+        TensorPoly f;
+        f.interpolate(k, vals, gl);
+        saye_poly(f, gx, gw, cq[c], cs[c], &S.n_splits);
+      }
+    }
+  for (int8_t l : S.loc) ++S.cells[l == INSIDE ? 0 : (l == INTERSECTED ? 1 : 2)];
+  auto cat_of = [&](int c) { return (int)category((unsigned)c, (unsigned)p, (unsigned)n); };
+  auto off_of = [&](int c) { return (int64_t)box_offset((unsigned)c, (unsigned)p, (unsigned)n); };
+  auto dofs = [&](int cx, int cy, int64_t *d) {
+    for (int iy = 0; iy < n1; ++iy)
+      for (int ix = 0; ix < n1; ++ix) d[iy * n1 + ix] = (off_of(cy) + iy) * N + off_of(cx) + ix;
+  };
+  std::vector<uint8_t> full_row((size_t)NN, 0);
+  int64_t d[100], e[100];
+  for (int cy = 0; cy < n; ++cy)
+    for (int cx = 0; cx < n; ++cx)
+      if (S.loc[(size_t)cy * n + cx] != INSIDE) {
+        dofs(cx, cy, d);
+        for (int i = 0; i < nd; ++i) full_row[(size_t)d[i]] = 1;
+      }
+  for (int64_t r = 0; r < NN; ++r)
+    if (full_row[(size_t)r]) S.zero_rows.push_back(r);
+  Slots C, M, K;
+  C.init(2, N, p + 1);
+  M.init(2, N, p + 1);
+  K.init(2, N, p + 1);
+  std::vector<Trip> ff, fg, ev;
+  std::vector<double> val(nd), grx(nd), gry(nd);
+  auto eval = [&](int cx, int cy, double s, double t) {
+    Shapes sx, sy;
+    shapes_1d(p, cat_of(cx), s, sx);
+    shapes_1d(p, cat_of(cy), t, sy);
+    for (int iy = 0; iy < n1; ++iy)
+      for (int ix = 0; ix < n1; ++ix) {
+        const int i = iy * n1 + ix;
+        val[i] = sx.v[ix] * sy.v[iy];
+        grx[i] = sx.d[ix] * sy.v[iy] / h;
+        gry[i] = sx.v[ix] * sy.d[iy] / h;
+      }
+  };
+  const double gd = S.nitsche / h;
+  for (int cy = 0; cy < n; ++cy)
+    for (int cx = 0; cx < n; ++cx) {
+      const size_t c = (size_t)cy * n + cx;
+      if (S.loc[c] == OUTSIDE) continue;
+      dofs(cx, cy, d);
+      const double x0 = S.lo + cx * h, y0 = S.lo + cy * h;
+      for (const QPoint &q : cq[c]) {
+        eval(cx, cy, q.s, q.t);
+        const double jxw = q.w * h * h;
+        const int64_t qi = (int64_t)S.qw.size();
+        S.qx.push_back(x0 + q.s * h);
+        S.qx.push_back(y0 + q.t * h);
+        S.qw.push_back(jxw);
+        for (int i = 0; i < nd; ++i) {
+          ff.push_back({d[i], qi, val[i] * jxw});
+          ev.push_back({qi, d[i], val[i]});
+          const bool crow = S.loc[c] == INTERSECTED || full_row[(size_t)d[i]];
+          for (int j = 0; j < nd; ++j) {
+            const double gg = grx[i] * grx[j] + gry[i] * gry[j];
+            if (crow) C.add(d[i], d[j], -gg * jxw);
+            M.add(d[i], d[j], val[i] * val[j] * jxw);
+            K.add(d[i], d[j], gg * jxw);
+          }
+        }
+      }
+      for (const SPoint &sp : cs[c]) {
+        eval(cx, cy, sp.s, sp.t);
+        const double jxw = sp.w * h;
+        const int64_t si = (int64_t)S.sx.size() / 2;
+        S.sx.push_back(x0 + sp.s * h);
+        S.sx.push_back(y0 + sp.t * h);
+        S.sn.push_back(sp.nx);
+        S.sn.push_back(sp.ny);
+        for (int i = 0; i < nd; ++i) {
+          const double dni = grx[i] * sp.nx + gry[i] * sp.ny;
+          fg.push_back({d[i], si, (gd * val[i] - dni) * jxw});
+          for (int j = 0; j < nd; ++j) {
+            const double dnj = grx[j] * sp.nx + gry[j] * sp.ny;
+            const double a = (-dni * val[j] - val[i] * dnj + gd * val[i] * val[j]) * jxw;
+            C.add(d[i], d[j], -a);
+            K.add(d[i], d[j], a);
+          }
+        }
+      }
+    }
+  // ghost penalty faces (mass.h:86-105, stiffness.h:80-98, 330-395): QGauss(p+1)
+  // on every face of a non-outside cell to a neighbour where one of the two is
+  // intersected and the other not outside, visited from both cells
+  std::map<int64_t, std::vector<double>> jump;
+  for (int cy = 0; cy < n; ++cy)
+    for (int cx = 0; cx < n; ++cx) {
+      const int lc = S.loc[(size_t)cy * n + cx];
+      if (lc == OUTSIDE) continue;
+      for (int f = 0; f < 4; ++f) {
+        const int axis = f / 2, side = f % 2;
+        const int nx = cx + (axis == 0 ? 2 * side - 1 : 0), ny = cy + (axis == 1 ? 2 * side - 1 : 0);
+        if (nx < 0 || nx >= n || ny < 0 || ny >= n) continue;
+        const int ln = S.loc[(size_t)ny * n + nx];
+        if (!((lc == INTERSECTED && ln != OUTSIDE) || (ln == INTERSECTED && lc != OUTSIDE))) continue;
+        jump.clear();
+        dofs(cx, cy, d);
+        dofs(nx, ny, e);
+        for (int q = 0; q < n1; ++q) {
+          // [d phi / dx_axis] at face point q: from the cell minus from the neighbour
+          const double sc = axis == 0 ? (double)side : gx[q], tc = axis == 0 ? gx[q] : (double)side;
+          const double sn = axis == 0 ? 1.0 - side : gx[q], tn = axis == 0 ? gx[q] : 1.0 - side;
+          eval(cx, cy, sc, tc);
+          for (int i = 0; i < nd; ++i) {
+            auto &jv = jump[d[i]];
+            jv.resize(n1, 0.0);
+            jv[q] += axis == 0 ? grx[i] : gry[i];
+          }
+          eval(nx, ny, sn, tn);
+          for (int i = 0; i < nd; ++i) {
+            auto &jv = jump[e[i]];
+            jv.resize(n1, 0.0);
+            jv[q] -= axis == 0 ? grx[i] : gry[i];
+          }
+        }
+        for (const auto &a : jump)
+          for (const auto &b : jump) {
+            double J = 0.0;
+            for (int q = 0; q < n1; ++q) J += a.second[q] * b.second[q] * gw[q] * h;
+            C.add(a.first, b.first, -0.5 * S.gA * h * J);
+            if (S.gM >= 0.0) M.add(a.first, b.first, 0.5 * S.gM * h * h * h * J);
+            K.add(a.first, b.first, 0.5 * S.gA * h * h * h * J);
+          }
+      }
+    }
+  C.csr(S.c_rp, S.c_ci, S.c_v, false);
+  M.csr(S.m_rp, S.m_ci, S.m_v, true);
+  K.csr(S.s_rp, S.s_ci, S.s_v, true);
+  triplets_csr(ff, NN, S.ff_rp, S.ff_ci, S.ff_v);
+  triplets_csr(fg, NN, S.fg_rp, S.fg_ci, S.fg_v);
+  triplets_csr(ev, (int64_t)S.qw.size(), S.e_rp, S.e_ci, S.e_v);
+}
+
 }  // namespace
 
 extern "C" {
@@ -327,14 +467,18 @@ extern "C" {
 int64_t gdmh_band_cholesky(int64_t n, const int64_t *rp, const uint32_t *ci, const double *v, double alpha,
                            const int64_t *rp2, const uint32_t *ci2, const double *v2, std::vector<double> &lband);
 
-int gdmh_cut_wave_create(int p, int n_sub, double lo, double hi, int ls_degree, const double *ls_values,
+int gdmh_cut_wave_create(int dim, int p, int n_sub, double lo, double hi, int ls_degree, const double *ls_values,
                          double gamma_M, double gamma_A, double nitsche, gdm_cut_wave_system **out, char *err,
                          size_t err_len) {
   try {
-    if (!out || !ls_values || p < 1 || p > 9 || p % 2 == 0 || n_sub < p || !(hi > lo) || ls_degree < 1 ||
-        ls_degree > 9)
-      throw std::invalid_argument("cut_wave: invalid arguments (p odd in [1, 9], n_sub >= p, hi > lo, 1 <= k <= 9)");
+    if (!out || !ls_values || (dim != 1 && dim != 2) || p < 1 || p > 9 || p % 2 == 0 || n_sub < p || !(hi > lo) ||
+        ls_degree < 1 || ls_degree > 9)
+      throw std::invalid_argument(
+          "cut_wave: invalid arguments (dim 1 or 2, p odd in [1, 9], n_sub >= p, hi > lo, 1 <= k <= 9)");
+    if (dim == 2 && (int64_t)(n_sub + 1) * (n_sub + 1) > (int64_t)1 << 31)
+      throw std::invalid_argument("cut_wave: mesh too large for 32-bit column indices");
     auto *S = new gdm_cut_wave_system();
+    S->dim = dim;
     S->p = p;
     S->n = n_sub;
     S->k = ls_degree;
@@ -344,7 +488,10 @@ int gdmh_cut_wave_create(int p, int n_sub, double lo, double hi, int ls_degree, 
     S->gA = gamma_A;
     S->nitsche = nitsche;
     try {
-      assemble(*S, ls_values);
+      if (dim == 1)
+        assemble1d(*S, ls_values);
+      else
+        assemble2d(*S, ls_values);
     } catch (...) {
       delete S;
       throw;
@@ -359,9 +506,9 @@ int gdmh_cut_wave_create(int p, int n_sub, double lo, double hi, int ls_degree, 
 
 void gdmh_cut_wave_info(const gdm_cut_wave_system *S, int64_t *n_dofs, int64_t *n_quad, int64_t *n_surface,
                         int64_t *cells) {
-  *n_dofs = S->n + 1;
-  *n_quad = (int64_t)S->qx.size();
-  *n_surface = (int64_t)S->sx.size();
+  *n_dofs = S->dim == 1 ? S->n + 1 : (int64_t)(S->n + 1) * (S->n + 1);
+  *n_quad = (int64_t)S->qw.size();
+  *n_surface = (int64_t)S->sx.size() / S->dim;
   for (int q = 0; q < 3; ++q) cells[q] = S->cells[q];
 }
 
@@ -387,6 +534,8 @@ void gdmh_cut_wave_points(const gdm_cut_wave_system *S, const double **qx, const
   *zero_rows = S->zero_rows.data();
   *n_zero = (int64_t)S->zero_rows.size();
 }
+
+int gdmh_cut_wave_splits(const gdm_cut_wave_system *S) { return S->n_splits; }
 
 void gdmh_cut_wave_destroy(gdm_cut_wave_system *S) { delete S; }
 

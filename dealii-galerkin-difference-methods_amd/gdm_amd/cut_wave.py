@@ -1,7 +1,8 @@
-"""The cut-cell wave / heat application on the device: the
-reference's applications/wave at dim = 1 -- a GDM line cut by the FE_Q(k)
-interpolant of a level set, location "inside", no domain Dirichlet data --
-through the C ABI "Cut-cell wave" entry points of include/gdm_hip.h.
+"""The cut-cell wave / heat / poisson application on the device (SURVEY §8
+f1): the reference's applications/wave at dim = 1 and 2 -- a GDM line or
+square cut by the FE_Q(k) interpolant of a level set, location "inside", no
+domain Dirichlet data -- through the C ABI "Cut-cell wave" entry points of
+include/gdm_hip.h.
 
   CutWave            StiffnessMatrixOperator::compute_rhs
                      (wave/stiffness.h:42-407) = uncut 1D wave stencil of
@@ -11,16 +12,16 @@ through the C ABI "Cut-cell wave" entry points of include/gdm_hip.h.
                      mass / (M + dt K) solves (wave/problem.h:457-502)
   CutWaveProblem     WaveProblem::run (wave/problem.h:39-346): wave-rk,
                      heat-rk (RK_CLASSIC_FOURTH_ORDER + DiscreteTime, the
-                     stages device-resident) and heat-impl (backward Euler
-                     u <- (M + dt K)^-1 (M u + dt F(t + dt))), with the
-                     postprocess table (counter, t, L2, L1, Linf) of
-                     problem.h:504-590
-  preset(name)       wave-app.cc:62-285 at dim = 1 ("wave", "heat-rk",
-                     "heat-impl")
+                     stages device-resident), heat-impl (backward Euler
+                     u <- (M + dt K)^-1 (M u + dt F(t + dt))) and poisson
+                     (u = K^-1 F, problem.h:46-71), with the postprocess
+                     table (counter, t, L2, L1, Linf) of problem.h:504-615
+  preset(name, dim)  wave-app.cc:13-347: "wave", "heat-rk", "heat-impl"
+                     (dim 1, 2) and "step85" (dim 2)
 
-f(x, t), g(x, t) and the exact solution are the caller's functions (the
-reference's Function::value calls), evaluated on the host at the quadrature
-and surface points and uploaded, as CutAdvectionProblem does for its
+f, g and the exact solution are the caller's functions of (x, t) in 1D and
+(x, y, t) in 2D (the reference's Function::value calls), evaluated on the
+host at the quadrature and surface points and uploaded, as CutAdvectionProblem does for its
 boundary data.  Every operator runs in libgdm_hip.so; there is no CPU path.
 """
 import ctypes
@@ -51,23 +52,40 @@ def gauss_lobatto(n):
     return np.concatenate([[0.0], np.sort((r + 1.0) / 2.0), [1.0]])
 
 
-class CutWave:
-    """Device operators of the 1D cut wave / heat problem on [left, right].
+def call(fun, pts, t):
+    """fun(x, t) on 1D points [n], fun(x, y, t) on 2D points [n, 2]"""
+    return fun(pts, t) if pts.ndim == 1 else fun(pts[:, 0], pts[:, 1], t)
 
-    level_set: callable phi(x) (vectorised); its FE_Q(ls_degree) interpolant
-    (values at each cell's Gauss-Lobatto points) defines inside (< 0)."""
+
+class CutWave:
+    """Device operators of the cut wave / heat / poisson problem on
+    [left, right]^dim (dim 1 or 2).
+
+    level_set: callable phi(x) (1D) or phi(x, y) (2D), vectorised; its
+    FE_Q(ls_degree) interpolant (values at each cell's Gauss-Lobatto points)
+    defines inside (< 0)."""
 
     def __init__(self, fe_degree, n_subdivisions, left, right, level_set, ls_degree=None, ghost_parameter_M=0.5,
-                 ghost_parameter_A=0.5, nitsche=None, device=0):
+                 ghost_parameter_A=0.5, nitsche=None, device=0, dim=1):
         self._lib = _capi.load()
         self._h = ctypes.c_void_p()
+        if dim not in (1, 2):
+            raise GdmError("CutWave: dim must be 1 or 2")
+        self.dim = dim
         k = fe_degree if ls_degree is None else ls_degree
         self.h = (right - left) / n_subdivisions
         gl = gauss_lobatto(k + 1)
-        x = (left + np.arange(n_subdivisions) * self.h)[:, None] + gl[None, :] * self.h
-        ls = np.ascontiguousarray(np.asarray(level_set(x.reshape(-1)), dtype=np.float64))
+        x = (left + np.arange(n_subdivisions) * self.h)[:, None] + gl[None, :] * self.h  # [cell][a]
+        if dim == 1:
+            ls = level_set(x.reshape(-1))
+        else:  # [cy][cx][b][a]
+            X = np.broadcast_to(x[None, :, None, :], (n_subdivisions, n_subdivisions, k + 1, k + 1))
+            Y = np.broadcast_to(x[:, None, :, None], X.shape)
+            ls = level_set(X.reshape(-1), Y.reshape(-1))
+        ls = np.ascontiguousarray(np.asarray(ls, dtype=np.float64))
         gamma_D = 5.0 * fe_degree if nitsche is None else nitsche
-        check(self._lib.gdm_cut_wave_create(int(fe_degree), int(n_subdivisions), float(left), float(right), int(k),
+        check(self._lib.gdm_cut_wave_create(int(dim), int(fe_degree), int(n_subdivisions), float(left), float(right),
+                                            int(k),
                                             ls.ctypes.data_as(ctypes.c_void_p), float(ghost_parameter_M),
                                             float(ghost_parameter_A), float(gamma_D), int(device),
                                             ctypes.byref(self._h)), "gdm_cut_wave_create")
@@ -77,18 +95,25 @@ class CutWave:
               "gdm_cut_wave_info")
         self.n_dofs, self.n_quad, self.n_surface = nd.value, nq.value, ns.value
         self.cells = dict(inside=cells[0], intersected=cells[1], outside=cells[2])
-        self.qx, self.qw = np.zeros(max(self.n_quad, 1)), np.zeros(max(self.n_quad, 1))
-        self.sx, self.sn = np.zeros(max(self.n_surface, 1)), np.zeros(max(self.n_surface, 1))
+        self.qx, self.qw = np.zeros(max(self.n_quad, 1) * dim), np.zeros(max(self.n_quad, 1))
+        self.sx, self.sn = np.zeros(max(self.n_surface, 1) * dim), np.zeros(max(self.n_surface, 1) * dim)
         check(self._lib.gdm_cut_wave_points(self._h, *[a.ctypes.data_as(ctypes.c_void_p)
                                                         for a in (self.qx, self.qw, self.sx, self.sn)]),
               "gdm_cut_wave_points")
-        self.qx, self.qw = self.qx[:self.n_quad], self.qw[:self.n_quad]
-        self.sx, self.sn = self.sx[:self.n_surface], self.sn[:self.n_surface]
+        self.qx, self.qw = self.qx[:self.n_quad * dim], self.qw[:self.n_quad]
+        self.sx, self.sn = self.sx[:self.n_surface * dim], self.sn[:self.n_surface * dim]
+        if dim == 2:
+            self.qx, self.sx, self.sn = self.qx.reshape(-1, 2), self.sx.reshape(-1, 2), self.sn.reshape(-1, 2)
         op = ctypes.c_void_p()
         check(self._lib.gdm_cut_wave_op(self._h, ctypes.byref(op)), "gdm_cut_wave_op")
         self._op = op
         self.device = device
-        self.vertices = left + np.arange(n_subdivisions + 1) * self.h
+        xv = left + np.arange(n_subdivisions + 1) * self.h
+        if dim == 1:
+            self.vertices = xv
+        else:  # DoF order: x fastest
+            X, Y = np.meshgrid(xv, xv, indexing="xy")
+            self.vertices = np.stack([X.reshape(-1), Y.reshape(-1)], axis=1)
         import torch
 
         s = torch.cuda.current_stream(device).cuda_stream
@@ -131,6 +156,10 @@ class CutWave:
               "gdm_cut_wave_system_solve")
         return x
 
+    def stiffness_solve(self, rhs, x):
+        check(self._lib.gdm_cut_wave_stiffness_solve(self._h, _ptr(rhs), _ptr(x)), "gdm_cut_wave_stiffness_solve")
+        return x
+
     def eval_quadrature(self, u, vals):
         check(self._lib.gdm_cut_wave_eval(self._h, _ptr(u), _ptr(vals)), "gdm_cut_wave_eval")
         return vals
@@ -144,30 +173,48 @@ class CutWave:
         check(self._lib.gdm_synchronize(self._op), "gdm_synchronize")
 
 
-def preset(name):
-    """wave-app.cc parameter sets at dim = 1 (wave-app.cc:62-150 heat, :222-285
-    wave): FE degree 3, 40 cells on [-1.21, 1.21], SignedDistance::Sphere of
-    radius 1 in FE_Q(3), gamma_D = 5 p."""
-    sphere = lambda x: np.abs(x) - 1.0  # noqa: E731
+def preset(name, dim=1):
+    """wave-app.cc parameter sets (:13-57 step85, :62-150 heat, :215-262 wave):
+    FE degree 3, 40 cells per direction on [-1.21, 1.21], SignedDistance::Sphere
+    of radius 1 in FE_Q(3), gamma_D = 5 p."""
+    if dim == 1:
+        sphere = lambda x: np.abs(x) - 1.0  # noqa: E731
+    elif dim == 2:
+        sphere = lambda x, y: np.hypot(x, y) - 1.0  # noqa: E731
+    else:
+        raise GdmError("cut_wave.preset: dim must be 1 or 2")
+    base = dict(simulation=name, dim=dim, p=3, n=40, left=-1.21, right=1.21, level_set=sphere, nitsche=15.0)
     if name == "wave":
-        k = 1.5 * math.pi
-        ex = lambda x, t: np.cos(k * np.abs(x)) * math.cos(k * t)  # noqa: E731
-        return dict(simulation=name, p=3, n=40, left=-1.21, right=1.21, level_set=sphere,
-                    gamma_M=0.25 * math.sqrt(3.0), gamma_A=0.5 * math.sqrt(3.0), nitsche=15.0, f=None, g=ex,
-                    exact=ex, start_t=0.0, end_t=2.0, cfl=0.3, cfl_pow=1.0)
+        if dim == 1:
+            k = 1.5 * math.pi
+            ex = lambda x, t: np.cos(k * np.abs(x)) * math.cos(k * t)  # noqa: E731
+        else:
+            import scipy.special
+
+            k = 3.0 * math.pi
+            ex = lambda x, y, t: scipy.special.j0(k * np.hypot(x, y)) * math.cos(k * t)  # noqa: E731
+        return dict(base, gamma_M=0.25 * math.sqrt(3.0), gamma_A=0.5 * math.sqrt(3.0), f=None, g=ex, exact=ex,
+                    start_t=0.0, end_t=2.0, cfl=0.3, cfl_pow=1.0)
     if name in ("heat-rk", "heat-impl"):
-        ex = lambda x, t: x ** 9 * math.exp(-t)  # noqa: E731
-        f = lambda x, t: -x ** 7 * math.exp(-t) * (x * x + 72)  # noqa: E731
+        if dim == 1:
+            ex = lambda x, t: x ** 9 * math.exp(-t)  # noqa: E731
+            f = lambda x, t: -x ** 7 * math.exp(-t) * (x * x + 72)  # noqa: E731
+        else:
+            ex = lambda x, y, t: x ** 9 * y ** 8 * math.exp(-t)  # noqa: E731
+            f = lambda x, y, t: -x ** 7 * y ** 6 * math.exp(-t) * (x * x * y * y + 72 * y * y + 56 * x * x)  # noqa
         cfl, cfl_pow = (0.3 / 9.0, 2.0) if name == "heat-rk" else (0.3, 1.0)
-        return dict(simulation=name, p=3, n=40, left=-1.21, right=1.21, level_set=sphere, gamma_M=0.75,
-                    gamma_A=1.5, nitsche=15.0, f=f, g=ex, exact=ex, start_t=0.0, end_t=0.1, cfl=cfl,
+        return dict(base, gamma_M=0.75, gamma_A=1.5, f=f, g=ex, exact=ex, start_t=0.0, end_t=0.1, cfl=cfl,
                     cfl_pow=cfl_pow)
-    raise GdmError("cut_wave.preset: %r (1D presets: wave, heat-rk, heat-impl)" % (name,))
+    if name == "step85" and dim == 2:
+        ex = lambda x, y, t: 1.0 - (x * x + y * y - 1.0)  # noqa: E731  1 - 2/dim (|x|^2 - 1)
+        return dict(base, simulation="poisson", gamma_M=-1.0, gamma_A=0.5, f=lambda x, y, t: np.full_like(x, 4.0),
+                    g=lambda x, y, t: np.ones_like(x), exact=ex, start_t=0.0, end_t=0.1, cfl=0.3, cfl_pow=1.0)
+    raise GdmError("cut_wave.preset: %r at dim %d (wave, heat-rk, heat-impl; step85 at dim 2)" % (name, dim))
 
 
 class CutWaveProblem:
-    """WaveProblem::run (wave/problem.h:39-346) on the device for one of the
-    1D simulation types "wave" (wave-rk), "heat-rk", "heat-impl"."""
+    """WaveProblem<dim>::run (wave/problem.h:39-346) on the device for the
+    simulation types "wave" (wave-rk), "heat-rk", "heat-impl" and "poisson"."""
 
     def __init__(self, params, device=0):
         import torch
@@ -175,7 +222,8 @@ class CutWaveProblem:
         P = dict(params)
         self.P = P
         self.cw = CutWave(P["p"], P["n"], P["left"], P["right"], P["level_set"], ghost_parameter_M=P["gamma_M"],
-                          ghost_parameter_A=P["gamma_A"], nitsche=P["nitsche"], device=device)
+                          ghost_parameter_A=P["gamma_A"], nitsche=P["nitsche"], device=device,
+                          dim=P.get("dim", 1))
         cw = self.cw
         self.sim = P["simulation"]
         self._torch = torch
@@ -198,10 +246,10 @@ class CutWaveProblem:
         P, cw = self.P, self.cw
         fq = gs = None
         if P["f"] is not None and cw.n_quad:
-            self._upload(P["f"](cw.qx, t), self._fq)
+            self._upload(call(P["f"], cw.qx, t), self._fq)
             fq = self._fq
         if P["g"] is not None and cw.n_surface:
-            self._upload(P["g"](cw.sx, t), self._gs)
+            self._upload(call(P["g"], cw.sx, t), self._gs)
             gs = self._gs
         return fq, gs
 
@@ -216,7 +264,7 @@ class CutWaveProblem:
         """(L2, L1, Linf) of u_h - u(t) over the inside quadrature (problem.h:504-590)"""
         cw = self.cw
         cw.eval_quadrature(self.u, self._vals)
-        e = self._vals[:cw.n_quad].cpu().numpy() - self.P["exact"](cw.qx, t)
+        e = self._vals[:cw.n_quad].cpu().numpy() - call(self.P["exact"], cw.qx, t)
         return (math.sqrt(float(np.sum(e * e * cw.qw))), float(np.sum(np.abs(e) * cw.qw)),
                 float(np.max(np.abs(e))) if len(e) else 0.0)
 
@@ -253,7 +301,15 @@ class CutWaveProblem:
     def run(self, max_steps=None):
         """the whole time loop; returns the postprocess table [(counter, t, L2, L1, Linf)]"""
         P, cw = self.P, self.cw
-        self._upload(P["exact"](cw.vertices, P["start_t"]), self.u)  # GDM::VectorTools::interpolate
+        if self.sim == "poisson":
+            # compute_rhs(rhs, 0, false, 0) + one stiffness solve (problem.h:46-71)
+            fq, gs = self._data(0.0)
+            cw.compute_rhs(None, fq, gs, self._r)
+            cw.stiffness_solve(self._r, self.u)
+            rows = [(0, 0.0) + self.postprocess(0.0)]
+            cw.synchronize()
+            return rows
+        self._upload(call(P["exact"], cw.vertices, P["start_t"]), self.u)  # GDM::VectorTools::interpolate
         if self.v is not None:
             self.v.zero_()
         dt = P["cfl"] * cw.h ** P["cfl_pow"]

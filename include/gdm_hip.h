@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 8
+#define GDM_HIP_ABI_VERSION 9
 
 enum gdm_status {
   GDM_OK = 0,
@@ -464,50 +464,59 @@ int gdm_cut_advection_mass_solve(gdm_cut_advection *c, const double *rhs, double
 int gdm_cut_advection_destroy(gdm_cut_advection *c);
 
 /* ------------------------------------------------------------------------
- * Cut-cell wave / heat (applications/wave, location inside, no
- * domain Dirichlet data, dim = 1: the "wave", "heat-rk" and "heat-impl"
- * presets of wave-app.cc): the device operators of the reference's wave
- * application on a GDM line cut by the FE_Q(k) interpolant of a level set.
+ * Cut-cell wave / heat / poisson (applications/wave, location
+ * inside, no domain Dirichlet data, dim 1 and 2: the "wave", "heat-rk",
+ * "heat-impl" and "step85" presets of wave-app.cc): the device operators of
+ * the reference's wave application on a GDM line / square cut by the FE_Q(k)
+ * interpolant of a level set (WaveProblem<dim>, wave/problem.h).
  *
  *   compute_rhs   rhs = [u != NULL] (Z S u + C u) + Ff fq + Fg gs
- *                 (wave/stiffness.h:42-407): S = the uncut 1D wave stencil
- *                 -(v', u') of the box (gdm_op kind wave), Z zeroes the rows
- *                 of the DoFs in the box of a cell that is not fully inside,
- *                 C = those rows of -(v', u')_inside in full + the surface
- *                 Nitsche terms (:205-259, gamma_D = nitsche) + the ghost
- *                 penalty -0.5 gamma_A h [v'][u'] (:386-392); Ff fq =
- *                 (v, f) with fq = f at the inside quadrature points, Fg gs =
- *                 the Nitsche data (gamma_D / h v - n v', g) with gs = g at
- *                 the surface points (either may be NULL: zero data).
- *                 Host assembly csrc/gdm_cut_wave.cpp, device CSR products.
- *   mass_apply    out = M u, M = (v, u)_inside + 0.5 gamma_M h^3 [v'][u'],
- *                 zero diagonals -> 1 (wave/mass.h:47-249)
+ *                 (wave/stiffness.h:42-407): S = the uncut wave stencil
+ *                 -(grad v, grad u) of the box (gdm_op kind wave), Z zeroes
+ *                 the rows of the DoFs in the box of a cell that is not fully
+ *                 inside, C = those rows of -(grad v, grad u)_inside in full
+ *                 + the surface Nitsche terms (:205-259, gamma_D = nitsche) +
+ *                 the ghost penalty -0.5 gamma_A h [d_n v][d_n u] on the faces
+ *                 (:330-395); Ff fq = (v, f) with fq = f at the inside
+ *                 quadrature points, Fg gs = the Nitsche data
+ *                 (gamma_D / h v - d_n v, g) with gs = g at the surface points
+ *                 (either may be NULL: zero data).  Host assembly
+ *                 csrc/gdm_cut_wave.cpp, device CSR products.
+ *   mass_apply    out = M u, M = (v, u)_inside + 0.5 gamma_M h^3 [d_n v][d_n u],
+ *                 zero diagonals -> 1 (wave/mass.h:47-249); gamma_M < 0 (the
+ *                 reference's "not set", e.g. step85): no mass matrix
  *   mass_solve    x = M^-1 rhs (banded Cholesky: host factor, device
  *                 triangular solves; wave/problem.h:457-502)
- *   system_solve  x = (M + dt K)^-1 rhs, K the stiffness matrix of heat-impl
- *                 (stiffness.h:602-800: (v', u')_inside + surface Nitsche +
- *                 0.5 gamma_A h^3 [v'][u']); refactored when dt changes
+ *   system_solve  x = (M + dt K)^-1 rhs, K the assembled stiffness matrix
+ *                 (stiffness.h:602-800: (grad v, grad u)_inside + surface
+ *                 Nitsche + 0.5 gamma_A h^3 [d_n v][d_n u], zero diagonals ->
+ *                 1; heat-impl); refactored when dt changes
+ *   stiffness_solve  x = K^-1 rhs (the "poisson" simulation type, problem.h:46-71)
  *   eval          vals = u_h at the inside quadrature points (the
- *                 postprocess of problem.h:504-590 reduces them with the
+ *                 postprocess of problem.h:504-615 reduces them with the
  *                 exact solution and the weights from gdm_cut_wave_points)
- * ls_values: [n_sub][k + 1] values of the level set at the Gauss-Lobatto
- * support points of each cell (the FE_Q(k) interpolant; cells with all
- * values < 0 inside, all > 0 outside, otherwise intersected).
- * Vectors: device pointers (n_dofs, n_quad, n_surface doubles).
+ * ls_values: per cell (lexicographic, x fastest) the level set at its
+ * (k + 1)^dim Gauss-Lobatto support points (x fastest): the FE_Q(k)
+ * interpolant.  Cells are classified by the signs of its Bernstein
+ * coefficients (NonMatching::MeshClassifier); intersected cells get deal.II's
+ * QuadratureGenerator (Saye) on the cell polynomial.  DoFs: vertices,
+ * lexicographic (x fastest).  Vectors: device pointers (n_dofs, n_quad,
+ * n_surface doubles).
  * ------------------------------------------------------------------------ */
 typedef struct gdm_cut_wave gdm_cut_wave;
-int gdm_cut_wave_create(int fe_degree, int n_subdivisions, double left, double right, int ls_degree,
+int gdm_cut_wave_create(int dim, int fe_degree, int n_subdivisions, double left, double right, int ls_degree,
                         const double *ls_values, double gamma_M, double gamma_A, double nitsche, int device,
                         gdm_cut_wave **out);
 /* cells[3] = inside, intersected, outside */
 int gdm_cut_wave_info(const gdm_cut_wave *c, int64_t *n_dofs, int64_t *n_quad, int64_t *n_surface, int64_t *cells);
-/* host arrays: quadrature points x and JxW [n_quad], surface points x and normals [n_surface] */
+/* host arrays: quadrature points [n_quad][dim] and JxW [n_quad], surface points and unit normals [n_surface][dim] */
 int gdm_cut_wave_points(const gdm_cut_wave *c, double *qx, double *qw, double *sx, double *sn);
 int gdm_cut_wave_op(gdm_cut_wave *c, gdm_op **op);
 int gdm_cut_wave_compute_rhs(gdm_cut_wave *c, const double *u, const double *fq, const double *gs, double *rhs);
 int gdm_cut_wave_mass_apply(gdm_cut_wave *c, const double *u, double *out);
 int gdm_cut_wave_mass_solve(gdm_cut_wave *c, const double *rhs, double *x);
 int gdm_cut_wave_system_solve(gdm_cut_wave *c, double dt, const double *rhs, double *x);
+int gdm_cut_wave_stiffness_solve(gdm_cut_wave *c, const double *rhs, double *x);
 int gdm_cut_wave_eval(gdm_cut_wave *c, const double *u, double *vals);
 int gdm_cut_wave_destroy(gdm_cut_wave *c);
 

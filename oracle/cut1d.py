@@ -6,7 +6,8 @@ reference root):
 
   * mesh + categories + DoF boxes      include/gdm/system.h:195-246, 404-424
   * level set: FE_Q(p) interpolant of SignedDistance::Sphere (|x| - r),
-    MeshClassifier (inside / outside / intersected)
+    MeshClassifier (signs of the interpolant's Bernstein coefficients:
+    inside / outside / intersected)
                                        applications/wave/include/gdm/wave/discretization.h:82-99
   * NonMatching::FEValues in 1D: QGauss(p+1) on the inside part of a cut
     cell, one surface point at the root with weight 1 and the level-set
@@ -124,9 +125,13 @@ class Cut1D:
         x0 = self.xv[c]
         # FE_Q(k) interpolant of the level set on the cell (Lagrange through GL points)
         vals = np.array([self.level_set(x0 + s * self.h) for s in self.gl])
-        if np.all(vals < 0):
+        # MeshClassifier: signs of the Bernstein coefficients of the interpolant
+        k = len(self.gl) - 1
+        B = np.array([[math.comb(k, i) * s ** i * (1 - s) ** (k - i) for i in range(k + 1)] for s in self.gl])
+        bern = np.linalg.solve(B, vals)
+        if np.all(bern < 0):
             loc = self.INSIDE
-        elif np.all(vals > 0):
+        elif np.all(bern > 0):
             loc = self.OUTSIDE
         else:
             loc = self.INTERSECTED

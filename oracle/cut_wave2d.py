@@ -17,8 +17,11 @@ and "step85" (poisson) at dim = 2 (paths relative to the reference root):
         by the vertex values; gradient bounds from the Hessian at the centre;
         definite if the value bounds exclude [-1e-11, 1e-11]
       - height direction: the largest lower bound of |df/dx_i| (first of
-        equal ones), used if > 1e-11; else the box is split in halves along
-        its longest side (at most 4 splits), then the midpoint rule
+        equal ones), used if > 1e-11; ties within 1e-12 relative (cells
+        symmetric about a diagonal, where deal.II's choice is decided by
+        round-off) take direction 0 unless tie_hdir overrides them;
+        else the box is split in halves along its longest side (at most 4
+        splits), then the midpoint rule
       - the cross-section split at the roots of the level set restricted to
         the bottom and top faces (RootFinder: sign change at the ends ->
         root; else Taylor bounds, up to 2 interval halvings), QGauss(p+1) per
@@ -167,11 +170,12 @@ class QGen:
     """QuadratureGenerator<2> for one TensorPoly on a box in reference
     coordinates: inside [(s, t, w)], surface [(s, t, w, normal)]."""
 
-    def __init__(self, f, qx, qw):
-        self.f, self.qx, self.qw = f, qx, qw
+    def __init__(self, f, qx, qw, tie=0):
+        self.f, self.qx, self.qw, self.tie = f, qx, qw, tie
         self.inside, self.surface = [], []
         self.n_splits = 0
         self.n_midpoint = 0
+        self.n_ties = 0
 
     def _tensor(self, lo, hi):
         L0, L1 = hi[0] - lo[0], hi[1] - lo[1]
@@ -207,7 +211,12 @@ class QGen:
         for i in range(2):
             dg = abs(H[i, 0]) * dx[0] + abs(H[i, 1]) * dx[1]
             low.append(_lower_abs(g[i] - dg, g[i] + dg))
-        hdir = 0 if low[0] >= low[1] else 1
+        # first of equal ones; equal within 1e-12 relative (cells symmetric about a diagonal tie up to round-off)
+        if abs(low[1] - low[0]) <= 1e-12 * max(low):
+            hdir = self.tie
+            self.n_ties += 1
+        else:
+            hdir = 1 if low[1] > low[0] else 0
         if low[hdir] > LIMIT:
             self._height(hdir, lo, hi)
         elif n_box_splits < MAX_BOX_SPLITS:
@@ -274,7 +283,7 @@ class CutWave2D:
     """The wave application's discretization on [left, right]^2 (GDM degree
     p, level set FE_Q(k) of |x| - 1)."""
 
-    def __init__(self, p=3, n=40, left=-1.21, right=1.21, k=None, level_set=None):
+    def __init__(self, p=3, n=40, left=-1.21, right=1.21, k=None, level_set=None, tie_hdir=None):
         self.p, self.n = p, n
         self.k = p if k is None else k
         self.h = (right - left) / n
@@ -291,6 +300,7 @@ class CutWave2D:
         self.loc = np.zeros((n, n), dtype=int)
         self.quad = {}
         self.n_splits = self.n_midpoint = 0
+        self.ties = []  # cells whose height direction was a tie
         self.ls_values = np.zeros((n, n, self.k + 1, self.k + 1))  # [cy, cx, b (t), a (s)]
         for cy in range(n):
             for cx in range(n):
@@ -304,8 +314,10 @@ class CutWave2D:
                     self.loc[cy, cx] = OUTSIDE
                 else:
                     self.loc[cy, cx] = INTERSECTED
-                    q = QGen(TensorPoly(A, vals), self.qx, self.qw)
+                    q = QGen(TensorPoly(A, vals), self.qx, self.qw, (tie_hdir or {}).get((cx, cy), 0))
                     q.generate((0.0, 0.0), (1.0, 1.0))
+                    if q.n_ties:
+                        self.ties.append((cx, cy))
                     self.n_splits += q.n_splits
                     self.n_midpoint += q.n_midpoint
                     self.quad[(cx, cy)] = (q.inside, q.surface)

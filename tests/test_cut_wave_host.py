@@ -34,7 +34,7 @@ def _lib():
 
     L = gdm_amd.load()
     P, I64, D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_double
-    L.gdmh_cut_wave_create.argtypes = [ctypes.c_int, ctypes.c_int, D, D, ctypes.c_int, P, D, D, D,
+    L.gdmh_cut_wave_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, D, D, ctypes.c_int, P, D, D, D,
                                        ctypes.POINTER(P), ctypes.c_char_p, ctypes.c_size_t]
     L.gdmh_cut_wave_info.argtypes = [P] + [ctypes.POINTER(I64)] * 3 + [P]
     L.gdmh_cut_wave_csr.argtypes = [P, ctypes.c_int] + [ctypes.POINTER(ctypes.c_void_p)] * 3
@@ -59,7 +59,7 @@ def host_system(prm):
     ls = np.ascontiguousarray((np.abs(x) - 1.0).reshape(-1))
     S = ctypes.c_void_p()
     err = ctypes.create_string_buffer(256)
-    assert L.gdmh_cut_wave_create(p, n, left, right, p, ls.ctypes.data, prm["gamma_M"], prm["gamma_A"],
+    assert L.gdmh_cut_wave_create(1, p, n, left, right, p, ls.ctypes.data, prm["gamma_M"], prm["gamma_A"],
                                   prm["nitsche"], ctypes.byref(S), err, 256) == 0, err.value
     try:
         nd, nq, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

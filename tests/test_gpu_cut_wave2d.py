@@ -1,0 +1,75 @@
+"""The 2D cut-cell wave application on the device (gdm_amd.CutWave /
+CutWaveProblem with dim = 2: include/gdm_hip.h "Cut-cell wave") against the
+reference's own application goldens applications/wave/tests/wave_1.output
+(wave-rk, 111 steps on the 40 x 40 mesh cut by the FE_Q(3) circle) and
+step85_0.output (poisson), with the tolerances of
+tests/test_cut_wave2d_golden.py; and the device compute_rhs against the 2D
+oracle's assembled operator.  The host assembly is checked piece by piece in
+tests/test_cut_wave2d_host.py."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+REF = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_outputs.json")))["wave_app"]["cases"]
+
+import cut_wave2d as W  # noqa: E402
+from test_cut_wave2d_golden import WAVE_1_RTOL, _check_wave_1  # noqa: E402
+
+
+def test_wave_1_on_device():
+    from gdm_amd.cut_wave import CutWaveProblem, preset
+
+    prob = CutWaveProblem(preset("wave", dim=2))
+    m = W.CutWave2D()
+    assert prob.cw.cells == dict(inside=int((m.loc == W.INSIDE).sum()), intersected=int((m.loc == W.INTERSECTED).sum()),
+                                 outside=int((m.loc == W.OUTSIDE).sum()))
+    _check_wave_1(prob.run(), WAVE_1_RTOL)
+
+
+def test_step85_on_device():
+    from gdm_amd.cut_wave import CutWaveProblem, preset
+
+    rows = CutWaveProblem(preset("step85", dim=2)).run()
+    assert len(rows) == 1 and rows[0][:2] == (0, 0.0)
+    np.testing.assert_allclose(rows[0][2:], REF["step85_0"]["steps"][0][2:], rtol=0, atol=2e-12)
+
+
+def test_compute_rhs_and_mass_vs_oracle():
+    """device compute_rhs (Z S u + C u + Fg g) and M^-1 against the oracle's
+    assembled operator -A u + Fg g and its sparse LU, random u"""
+    import scipy.sparse.linalg as spla
+
+    from gdm_amd.cut_wave import CutWave, preset
+
+    P = preset("wave", dim=2)
+    cw = CutWave(P["p"], P["n"], P["left"], P["right"], P["level_set"], ghost_parameter_M=P["gamma_M"],
+                 ghost_parameter_A=P["gamma_A"], nitsche=P["nitsche"], dim=2)
+    m = W.CutWave2D()
+    ops = m.matrices(P["gamma_M"], P["gamma_A"], P["nitsche"])
+    assert cw.n_quad == len(ops["q"]) and cw.n_surface == len(ops["s"])
+    rng = np.random.default_rng(5)
+    u = rng.uniform(-1, 1, cw.n_dofs)
+    gs = rng.uniform(-1, 1, cw.n_surface)
+    out = cw.new_vector()
+    cw.compute_rhs(torch.from_numpy(u).cuda(), None, torch.from_numpy(gs).cuda(), out)
+    ref = -(ops["A"] @ u) + ops["Fg"] @ gs
+    assert np.abs(out.cpu().numpy() - ref).max() <= 1e-12 * np.abs(ref).max()
+    x = cw.new_vector()
+    cw.mass_solve(torch.from_numpy(ref).cuda(), x)
+    # cond(M) = 6e7 (small cut cells): compare within cond * eps, and the residual
+    xg = x.cpu().numpy()
+    xr = spla.splu(ops["M"].tocsc()).solve(ref)
+    assert np.linalg.norm(xg - xr) <= 1e-7 * np.linalg.norm(xr)
+    assert np.linalg.norm(ops["M"] @ xg - ref) <= 1e-10 * np.linalg.norm(ref)
+    Mu = cw.new_vector()
+    cw.mass_apply(torch.from_numpy(xr).cuda(), Mu)
+    assert np.abs(Mu.cpu().numpy() - ops["M"] @ xr).max() <= 1e-12 * np.abs(ref).max()
