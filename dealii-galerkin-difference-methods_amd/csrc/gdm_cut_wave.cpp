@@ -1,18 +1,21 @@
-// gdm_cut_wave.cpp -- host assembly of the cut-cell parts of the 1D wave /
-// heat application (applications/wave, location "inside", no domain
+// gdm_cut_wave.cpp -- host assembly of the cut-cell parts of the wave /
+// heat / poisson application (applications/wave, location "inside", no domain
 // Dirichlet data: wave-app.cc presets "wave", "heat-rk", "heat-impl" at
-// dim = 1) for the device operator of gdm_capi.cpp ("Cut-cell wave" in
-// include/gdm_hip.h).
+// dim = 1 and 2, "step85" at dim = 2) for the device operator of gdm_capi.cpp
+// ("Cut-cell wave" in include/gdm_hip.h).
 //
-// The mesh is a GDM line [left, right] cut by the FE_Q(k) interpolant of a
-// level set (wave/discretization.h:82-99: SignedDistance::Sphere into FE_Q(k),
-// MeshClassifier): the caller gives the interpolant's values at the k + 1
-// Gauss-Lobatto support points of every cell.  Per cell: inside (all values
-// < 0), outside (all > 0) or intersected; an intersected cell's inside part
-// is found from the roots of its interpolant (sign changes on a 64-interval
-// grid refined by bisection to machine precision) and carries QGauss(p+1) on
-// each inside sub-interval and one surface point per root (weight 1, normal
-// = sign of the interpolant's slope) -- NonMatching::FEValues in 1D.
+// The mesh is a GDM line [left, right] or square [left, right]^2 cut by the
+// FE_Q(k) interpolant of a level set (wave/discretization.h:78-93:
+// SignedDistance::Sphere into FE_Q(k), MeshClassifier): the caller gives the
+// interpolant's values at the (k + 1)^dim Gauss-Lobatto support points of
+// every cell.  Per cell: inside / outside / intersected by the signs of the
+// interpolant's Bernstein coefficients (MeshClassifier).  1D: an intersected
+// cell's inside part comes from the roots of its interpolant (sign changes on
+// a 64-interval grid refined by bisection to machine precision), QGauss(p+1)
+// on each inside sub-interval and one surface point per root (weight 1,
+// normal = sign of the slope).  2D: deal.II's QuadratureGenerator on the
+// cell's tensor-product polynomial (saye_poly, gdm_cut.cpp) -- NonMatching::
+// FEValues.
 //
 // The device evaluates StiffnessMatrixOperator::compute_rhs
 // (wave/stiffness.h:42-407) as
@@ -20,23 +23,26 @@
 // with S the uncut 1D wave stencil of the box (-(v', u'), gdm_op kind wave),
 // Z zeroing the rows of DoFs in the box of a cell that is not fully inside,
 // and the sparse parts assembled here:
-//   C   those rows of -(v', u')_inside in full, the surface Nitsche terms
-//       -(-n v' u - n u' v + gamma_D / h v u) (stiffness.h:205-259) of the
-//       cut cells, and the ghost penalty -0.5 gamma_A h [v'][u'] (h^1 in the
-//       right-hand side, stiffness.h:386-392) on the faces of intersected
-//       cells with a non-outside neighbour, visited from both cells;
+//   C   those rows of -(grad v, grad u)_inside in full, the surface Nitsche
+//       terms -(-d_n v u - d_n u v + gamma_D / h v u) (stiffness.h:205-259)
+//       of the cut cells, and the ghost penalty -0.5 gamma_A h [d_n v][d_n u]
+//       (h^1 in the right-hand side, stiffness.h:386-392; QGauss(p+1) on 2D
+//       faces) on the faces of intersected cells with a non-outside
+//       neighbour, visited from both cells;
 //   Ff  (v, f): column q = the inside quadrature point q (JxW folded in);
 //   Fg  the Nitsche data g (gamma_D / h v - n v'): column s = surface point s.
-// Mass (wave/mass.h:47-249): (v, u)_inside + 0.5 gamma_M h^3 [v'][u'], zero
-// diagonals -> 1; stiffness matrix of heat-impl (stiffness.h:602-800):
-// (v', u')_inside + surface Nitsche + 0.5 gamma_A h^3 [v'][u'], zero
-// diagonals -> 1.  Both are small band matrices: the mass solve and the
-// (M + dt S) solve of heat-impl are exact banded Cholesky solves (factor
-// here, triangular solves on the device), the reference's 1D solves
-// converge in 1-2 preconditioned CG steps to 1e-14 (wave_0.output).
+// Mass (wave/mass.h:47-249): (v, u)_inside + 0.5 gamma_M h^3 [d_n v][d_n u],
+// zero diagonals -> 1 (none when gamma_M < 0); stiffness matrix
+// (stiffness.h:602-800): (grad v, grad u)_inside + surface Nitsche +
+// 0.5 gamma_A h^3 [d_n v][d_n u], zero diagonals -> 1.  Both are band
+// matrices (half-bandwidth (p+1)(N+1) in 2D): the mass solve, the (M + dt K)
+// solve of heat-impl and the K solve of poisson are exact banded Cholesky
+// solves (factor here, triangular solves on the device); the reference's
+// solves converge in 2-3 AMG-preconditioned CG steps to 1e-14.
 // E (n_quad x N): shape values at the inside quadrature points, for the
-// postprocess (problem.h:504-590).  Test oracle: oracle/cut1d.py, pinned by
-// applications/wave/tests/{wave_0,heat_0,heat_1}.output.
+// postprocess (problem.h:504-615).  Test oracles: oracle/cut1d.py and
+// oracle/cut_wave2d.py, pinned by applications/wave/tests/{wave_0,heat_0,
+// heat_1,wave_1,step85_0}.output.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
