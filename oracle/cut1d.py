@@ -20,6 +20,11 @@ reference root):
     (GP, h^3 in the matrix)          .../wave/stiffness.h:602-800
   * wave-rk, heat-rk (RK_CLASSIC_FOURTH_ORDER + DiscreteTime), heat-impl
     (u <- (M + dt S)^-1 (M u + dt f))  .../wave/problem.h:39-346
+  * composite (heat-composite, wave-composite): an inside and an outside
+    field, each with its region's mass / stiffness / ghost penalty, domain
+    Dirichlet data by Nitsche on the boundary faces in its region (IV,
+    .../wave/stiffness.h:262-330), coupled by the interface terms of
+    compute_rhs(BlockVector) (:420-575)
   * postprocess: L2 / L1 / Linf error on the inside quadrature
                                        .../wave/problem.h:504-590
   * parameters of "wave", "heat-rk", "heat-impl"   applications/wave/wave-app.cc:62-285
@@ -28,7 +33,7 @@ The mass / system solves are exact (dense LU): the reference's CG with
 AMG / ILU to ReductionControl(1000, 1e-20, 1e-14) converges in 1-2 steps on
 these 41-DoF systems (the "[L] solved in N" lines), i.e. to the same values
 within 1e-14.  Pinned to applications/wave/tests/{wave_0,heat_0,heat_1}.output
-(tests/test_cut1d_golden.py); the level-set root is found by bisection to
+and {wave,heat}_composite_0.output (tests/test_cut1d_golden.py); the level-set root is found by bisection to
 machine precision where deal.II's root finder stops at its tolerance, a
 difference far below the 9 printed digits.
 """
@@ -147,10 +152,11 @@ class Cut1D:
             return r
 
         cell = dict(c=c, x0=x0, cat=self.category(c), off=self.offset(c), loc=loc, surface=[])
+        full = [(x0 + s * self.h, w * self.h) for s, w in zip(self.qx, self.qw)]
         if loc == self.INSIDE:
-            cell["q"] = [(x0 + s * self.h, w * self.h) for s, w in zip(self.qx, self.qw)]
+            cell["q"], cell["q_out"] = full, []
         elif loc == self.OUTSIDE:
-            cell["q"] = []
+            cell["q"], cell["q_out"] = [], full
         else:
             # roots of the interpolant in (0, 1): sign changes on a fine grid + bisection
             grid = np.linspace(0.0, 1.0, 65)
@@ -173,11 +179,14 @@ class Cut1D:
                             hi = mid
                     roots.append(0.5 * (lo + hi))
             pts = [0.0] + roots + [1.0]
-            q = []
+            q, q_out = [], []
             for a, b in zip(pts[:-1], pts[1:]):
+                seg = [(x0 + (a + (b - a) * s) * self.h, (b - a) * w * self.h) for s, w in zip(self.qx, self.qw)]
                 if phi(0.5 * (a + b)) < 0:  # inside sub-interval
-                    q += [(x0 + (a + (b - a) * s) * self.h, (b - a) * w * self.h) for s, w in zip(self.qx, self.qw)]
-            cell["q"] = q
+                    q += seg
+                else:
+                    q_out += seg
+            cell["q"], cell["q_out"] = q, q_out
             for r in roots:
                 # level-set normal (gradient direction) at the root, finite difference of the interpolant
                 e = 1e-7
@@ -200,22 +209,27 @@ class Cut1D:
         return cell["off"] + np.arange(self.p + 1)
 
     # -- ghost-penalty faces (mass.h:86-105 / stiffness.h:80-98) ------------
-    def gp_faces(self):
+    def gp_faces(self, location=-1):
         """(cell, neighbour, face point) for every (cell, face) pair the
-        reference visits; each interior face near a cut is visited from both
-        sides (the 0.5 factors)."""
+        reference visits for the field of `location` (INSIDE / OUTSIDE); each
+        interior face near a cut is visited from both sides (the 0.5 factors)."""
+        inv = -location
         out = []
         for c, cell in enumerate(self.cells):
-            if cell["loc"] == self.OUTSIDE:
+            if cell["loc"] == inv:
                 continue
             for f, nb in ((0, c - 1), (1, c + 1)):
                 if nb < 0 or nb >= self.n:
                     continue
                 nl = self.cells[nb]["loc"]
-                if (cell["loc"] == self.INTERSECTED and nl != self.OUTSIDE) or \
-                        (nl == self.INTERSECTED and cell["loc"] != self.OUTSIDE):
+                if (cell["loc"] == self.INTERSECTED and nl != inv) or \
+                        (nl == self.INTERSECTED and cell["loc"] != inv):
                     out.append((c, nb, self.xv[c + f]))
         return out
+
+    def region(self, cell, location):
+        """the cell's quadrature of the INSIDE or OUTSIDE region"""
+        return cell["q"] if location == self.INSIDE else cell["q_out"]
 
     def _jump_grad(self, c, nb, xf):
         """global DoF -> [dphi/dx] = (from cell c) - (from neighbour) at face xf"""
@@ -232,16 +246,16 @@ class Cut1D:
         return j
 
     # -- matrices -----------------------------------------------------------
-    def mass_matrix(self, gamma_M):
+    def mass_matrix(self, gamma_M, location=-1):
         M = np.zeros((self.N, self.N))
         for cell in self.cells:
-            if cell["loc"] == self.OUTSIDE:
+            if cell["loc"] == -location:
                 continue
             d = self.dofs(cell)
-            for x, jxw in cell["q"]:
+            for x, jxw in self.region(cell, location):
                 v = self.shapes(cell, x, 0)
                 M[np.ix_(d, d)] += np.outer(v, v) * jxw
-        for c, nb, xf in self.gp_faces():
+        for c, nb, xf in self.gp_faces(location):
             j = self._jump_grad(c, nb, xf)
             keys = list(j)
             for a in keys:
@@ -276,17 +290,18 @@ class Cut1D:
                 S[i, i] = 1.0
         return S
 
-    def rhs(self, u, t, impl, gamma_A, nitsche, f=None, g=None):
-        """StiffnessMatrixOperator::compute_rhs (wave/stiffness.h:42-407),
-        location inside, no domain Dirichlet data"""
+    def rhs(self, u, t, impl, gamma_A, nitsche, f=None, g=None, location=-1, g_domain=None):
+        """StiffnessMatrixOperator::compute_rhs_internal (wave/stiffness.h:42-407)
+        for the field of `location`: interface Dirichlet data g (II), domain
+        Dirichlet data g_domain on the boundary faces of that region (IV)"""
         r = np.zeros(self.N)
         for cell in self.cells:
-            if cell["loc"] == self.OUTSIDE:
+            if cell["loc"] == -location:
                 continue
             d = self.dofs(cell)
             ul = u[d]
             cv = np.zeros(self.p + 1)
-            for x, jxw in cell["q"]:
+            for x, jxw in self.region(cell, location):
                 v, gr = self.shapes(cell, x, 0), self.shapes(cell, x, 1)
                 if impl:
                     cv -= gr * (gr @ ul) * jxw
@@ -294,28 +309,64 @@ class Cut1D:
                     cv += f(x, t) * v * jxw
             if g is not None:
                 for xs, n in cell["surface"]:
+                    n = n if location == self.INSIDE else -n
                     v, gr = self.shapes(cell, xs, 0), self.shapes(cell, xs, 1)
                     uq, duq = v @ ul, gr @ ul
                     if impl:
                         cv -= (-n * gr * uq - n * duq * v + nitsche / self.h * v * uq)
                     cv += g(xs, t) * (nitsche / self.h * v - n * gr)
+            if g_domain is not None:
+                for xf, n in self.domain_faces(cell, location):
+                    v, gr = self.shapes(cell, xf, 0), self.shapes(cell, xf, 1)
+                    uq, duq = v @ ul, gr @ ul
+                    if impl:
+                        cv -= (-n * gr * uq - n * duq * v + nitsche / self.h * v * uq)
+                    cv += g_domain(xf, t) * (nitsche / self.h * v - n * gr)
             r[d] += cv
         if impl:
-            for c, nb, xf in self.gp_faces():
+            for c, nb, xf in self.gp_faces(location):
                 j = self._jump_grad(c, nb, xf)
                 ju = sum(j[a] * u[a] for a in j)
                 for a in j:
                     r[a] -= 0.5 * gamma_A * self.h * j[a] * ju
         return r
 
-    def errors(self, u, exact, t):
-        """problem.h:504-590: (L2, L1, Linf) over the inside quadrature"""
+    def domain_faces(self, cell, location):
+        """(point, outward normal) of the cell's faces on the domain boundary
+        that lie in the region of `location` (NonMatching::FEInterfaceValues
+        of the face: the level set's sign at the face point)"""
+        out = []
+        for xf, n, at in ((self.xv[0], -1.0, cell["c"] == 0), (self.xv[-1], 1.0, cell["c"] == self.n - 1)):
+            if at and np.sign(self.level_set(xf)) == location:
+                out.append((xf, n))
+        return out
+
+    def coupling(self, u0, u1, nitsche):
+        """the composite interface terms of compute_rhs(BlockVector)
+        (wave/stiffness.h:420-575): tau = nitsche / 2, [u] = u0 - u1,
+        {u'} = (u0' + u1') / 2 on the surface points of intersected cells"""
+        r0, r1 = np.zeros(self.N), np.zeros(self.N)
+        tau = 0.5 * nitsche
+        for cell in self.cells:
+            if cell["loc"] != self.INTERSECTED:
+                continue
+            d = self.dofs(cell)
+            for xs, n in cell["surface"]:
+                v, gr = self.shapes(cell, xs, 0), self.shapes(cell, xs, 1)
+                jump = v @ u0[d] - v @ u1[d]
+                avg = 0.5 * (gr @ u0[d] + gr @ u1[d])
+                r0[d] -= -0.5 * n * gr * jump - v * n * avg + tau / self.h * v * jump
+                r1[d] -= -0.5 * n * gr * jump + v * n * avg - tau / self.h * v * jump
+        return r0, r1
+
+    def errors(self, u, exact, t, location=-1):
+        """problem.h:504-590: (L2, L1, Linf) over the region's quadrature"""
         l2, l1, linf = 0.0, 0.0, 0.0
         for cell in self.cells:
-            if cell["loc"] == self.OUTSIDE:
+            if cell["loc"] == -location:
                 continue
             ul = u[self.dofs(cell)]
-            for x, jxw in cell["q"]:
+            for x, jxw in self.region(cell, location):
                 e = self.shapes(cell, x, 0) @ ul - exact(x, t)
                 l2 += e * e * jxw
                 l1 += abs(e) * jxw
@@ -345,6 +396,65 @@ def heat_params(kind):
     cfl, cfl_pow = (0.3 / 9.0, 2.0) if kind == "heat-rk" else (0.3, 1.0)
     return dict(p=3, n=40, left=-1.21, right=1.21, gamma_M=0.75, gamma_A=1.5, nitsche=15.0, g=ex, f=f, exact=ex,
                 start_t=0.0, end_t=0.1, cfl=cfl, cfl_pow=cfl_pow)
+
+
+def composite_params(kind):
+    """wave-app.cc:150-214 heat-composite (heat-rk), :263-330 wave-composite
+    (wave-rk): an inside and an outside field coupled across the interface,
+    domain Dirichlet data on the boundary faces, no interface data"""
+    if kind == "heat-composite":
+        P = heat_params("heat-rk")
+    else:
+        P = wave_params()
+    P = dict(P, g_domain=P["g"], g=None)
+    return P
+
+
+def run_composite(simulation, max_steps=None):
+    """WaveProblem<1>::run for "heat-composite" / "wave-composite": rows
+    [(counter, t, L2, L1, Linf)] alternating inside / outside
+    (problem.h:128-214 heat-rk, :346-433 wave-rk)"""
+    P = composite_params(simulation)
+    m = Cut1D(P["p"], P["n"], P["left"], P["right"], _sphere)
+    I, O_ = Cut1D.INSIDE, Cut1D.OUTSIDE
+    Minv = [np.linalg.inv(m.mass_matrix(P["gamma_M"], loc)) for loc in (I, O_)]
+    dt = P["cfl"] * m.h ** P["cfl_pow"]
+    time = DiscreteTime(P["start_t"], P["end_t"], dt)
+    N = m.N
+
+    def fields_rhs(t, u0, u1):
+        c0, c1 = m.coupling(u0, u1, P["nitsche"])
+        r = [m.rhs(u, t, True, P["gamma_A"], P["nitsche"], f=P["f"], location=loc, g_domain=P["g_domain"]) + c
+             for u, loc, c in ((u0, I, c0), (u1, O_, c1))]
+        return Minv[0] @ r[0], Minv[1] @ r[1]
+
+    rows = []
+
+    def post(t, u0, u1, counter):
+        rows.append((counter, t) + m.errors(u0, P["exact"], t, I))
+        rows.append((counter, t) + m.errors(u1, P["exact"], t, O_))
+
+    u = m.interpolate(P["exact"], P["start_t"])
+    post(0.0, u, u, 0)
+    if simulation == "wave-composite":
+        y = np.concatenate([u, u, np.zeros(N), np.zeros(N)])
+
+        def f(t, y):
+            a0, a1 = fields_rhs(t, y[:N], y[N:2 * N])
+            return np.concatenate([y[2 * N:3 * N], y[3 * N:], a0, a1])
+    else:
+        y = np.concatenate([u, u])
+
+        def f(t, y):
+            return np.concatenate(fields_rhs(t, y[:N], y[N:]))
+    n = 0
+    while not time.is_at_end() and (max_steps is None or n < max_steps):
+        t0, h = time.t, time.next_step_size()
+        y = rk4_step(f, t0, h, y)
+        n += 1
+        post(t0 + h, y[:N], y[N:2 * N], n)
+        time.advance()
+    return rows
 
 
 def run(simulation, max_steps=None):

@@ -1,6 +1,6 @@
 """The 1D cut-cell restatement of the reference's wave application
 (oracle/cut1d.py) against the reference's own application goldens
-applications/wave/tests/{wave_0,heat_0,heat_1}.output (parsed into
+applications/wave/tests/{wave_0,heat_0,heat_1,wave_composite_0,heat_composite_0}.output (parsed into
 tests/golden/reference_outputs.json by tests/golden/make_golden.py).
 
 These pin, for dim = 1 with the trivial 1D cut, the wave-rk loop
@@ -34,6 +34,23 @@ def test_wave_app_golden(case, simulation):
     for got, exp in zip(rows, ref["steps"]):
         assert got[0] == exp[0]
         assert abs(got[1] - exp[1]) <= 5.000001e-6  # printed %8.5f
+        np.testing.assert_allclose(got[2:], exp[2:], rtol=2e-8, atol=0)
+
+
+@pytest.mark.parametrize("case,simulation", [("wave_composite_0", "wave-composite"),
+                                             ("heat_composite_0", "heat-composite")])
+def test_wave_app_composite_golden(case, simulation):
+    """the composite presets: inside and outside fields with their own masses
+    and ghost penalties, domain Dirichlet data on the boundary faces, the
+    interface coupling of compute_rhs(BlockVector) (wave/stiffness.h:420-575);
+    rows alternate inside / outside"""
+    ref = REF[case]
+    assert ref["config"]["dim"] == 1
+    rows = cut1d.run_composite(simulation)
+    assert len(rows) == len(ref["steps"])
+    for got, exp in zip(rows, ref["steps"]):
+        assert got[0] == exp[0]
+        assert abs(got[1] - exp[1]) <= 5.000001e-6
         np.testing.assert_allclose(got[2:], exp[2:], rtol=2e-8, atol=0)
 
 
