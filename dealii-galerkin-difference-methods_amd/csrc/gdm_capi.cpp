@@ -2197,8 +2197,8 @@ int gdm_cut_advection_destroy(gdm_cut_advection *c) {
 struct gdm_cut_wave_system;
 extern "C" {
 int gdmh_cut_wave_create(int dim, int p, int n_sub, double lo, double hi, int ls_degree, const double *ls_values,
-                         double gamma_M, double gamma_A, double nitsche, gdm_cut_wave_system **out, char *err,
-                         size_t err_len);
+                         int location, int flags, double gamma_M, double gamma_A, double nitsche,
+                         gdm_cut_wave_system **out, char *err, size_t err_len);
 void gdmh_cut_wave_info(const gdm_cut_wave_system *S, int64_t *n_dofs, int64_t *n_quad, int64_t *n_surface,
                         int64_t *cells);
 void gdmh_cut_wave_csr(const gdm_cut_wave_system *S, int which, const int64_t **rp, const uint32_t **ci,
@@ -2252,12 +2252,13 @@ struct gdm_cut_wave {
   gdm_op *op = nullptr;
   int dim = 1;
   int64_t n_dofs = 0, n_quad = 0, n_surf = 0, cells[3] = {0, 0, 0};
-  DevCsr C, Ff, Fg, E, M;
+  DevCsr C, Ff, Fg, E, M, X;
+  bool coupled = false;
   int64_t *zrows = nullptr, n_zrows = 0;
   int64_t bw_m = -1, bw_a = -1, bw_k = -1;  // -1: no factor (no mass matrix when gamma_M < 0)
   double *lband_m = nullptr, *lband_a = nullptr, *lband_k = nullptr, dt_a = 0.0;
   void release() {
-    for (DevCsr *q : {&C, &Ff, &Fg, &E, &M}) q->release();
+    for (DevCsr *q : {&C, &Ff, &Fg, &E, &M, &X}) q->release();
     for (void *q : {(void *)zrows, (void *)lband_m, (void *)lband_a, (void *)lband_k})
       if (q) (void)hipFree(q);
     zrows = nullptr;
@@ -2272,16 +2273,16 @@ struct gdm_cut_wave {
 extern "C" {
 
 int gdm_cut_wave_create(int dim, int fe_degree, int n_subdivisions, double left, double right, int ls_degree,
-                        const double *ls_values, double gamma_M, double gamma_A, double nitsche, int device,
-                        gdm_cut_wave **out) {
+                        const double *ls_values, int location, int flags, double gamma_M, double gamma_A,
+                        double nitsche, int device, gdm_cut_wave **out) {
   if (!out || !ls_values) return fail(GDM_ERR_ARG, "NULL argument");
   *out = nullptr;
   GDM_GUARD_BEGIN
   auto *c = new gdm_cut_wave();
   try {
     char err[256] = {0};
-    if (gdmh_cut_wave_create(dim, fe_degree, n_subdivisions, left, right, ls_degree, ls_values, gamma_M, gamma_A,
-                             nitsche, &c->host, err, sizeof(err)) != 0) {
+    if (gdmh_cut_wave_create(dim, fe_degree, n_subdivisions, left, right, ls_degree, ls_values, location, flags,
+                             gamma_M, gamma_A, nitsche, &c->host, err, sizeof(err)) != 0) {
       delete c;
       return fail(GDM_ERR_ARG, err);
     }
@@ -2313,6 +2314,8 @@ int gdm_cut_wave_create(int dim, int fe_degree, int n_subdivisions, double left,
     c->Fg.upload(c->host, 2, c->n_dofs);
     c->E.upload(c->host, 3, c->n_quad);
     c->M.upload(c->host, 4, c->n_dofs);
+    c->coupled = (flags & GDM_CUT_WAVE_COUPLED) != 0;
+    if (c->coupled) c->X.upload(c->host, 6, c->n_dofs);
     const double *qx, *qw, *sx, *sn;
     const int64_t *zr;
     gdmh_cut_wave_points(c->host, &qx, &qw, &sx, &sn, &zr, &c->n_zrows);
@@ -2383,6 +2386,16 @@ int gdm_cut_wave_compute_rhs(gdm_cut_wave *c, const double *u, const double *fq,
   }
   if (fq && c->n_quad > 0) c->Ff.accum(fq, rhs, st);
   if (gs && c->n_surf > 0) c->Fg.accum(gs, rhs, st);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_wave_couple(gdm_cut_wave *c, const double *u_other, double *rhs) {
+  if (!c || !u_other || !rhs) return fail(GDM_ERR_ARG, "NULL argument");
+  if (!c->coupled) return fail(GDM_ERR_ARG, "gdm_cut_wave_couple: created without GDM_CUT_WAVE_COUPLED");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  c->X.accum(u_other, rhs, c->op->stream);
   return GDM_OK;
   GDM_GUARD_END
 }

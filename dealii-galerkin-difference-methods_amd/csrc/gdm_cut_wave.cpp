@@ -56,15 +56,17 @@
 
 struct gdm_cut_wave_system {
   int dim = 1, p = 0, n = 0, k = 0, n_splits = 0;
+  int location = -1, dirichlet = 1;  // the field's region (INSIDE -1 / OUTSIDE 1); Nitsche data: bit 0 interface, bit 1 domain
+  bool coupled = false;                  // composite: interface coupling to the other region's field
   double lo = 0.0, h = 0.0, gM = 0.0, gA = 0.0, nitsche = 0.0;
   std::vector<int8_t> loc;
   std::vector<double> qx, qw;  // inside quadrature: global coordinates [n][dim], JxW
   std::vector<double> sx, sn;  // surface points: global coordinates [n][dim], normal [n][dim]
   std::vector<int64_t> zero_rows;
-  // CSR: C [N][N], Ff [N][nq], Fg [N][ns], E [nq][N], M [N][N], S [N][N]
-  std::vector<int64_t> c_rp, ff_rp, fg_rp, e_rp, m_rp, s_rp;
-  std::vector<uint32_t> c_ci, ff_ci, fg_ci, e_ci, m_ci, s_ci;
-  std::vector<double> c_v, ff_v, fg_v, e_v, m_v, s_v;
+  // CSR: C [N][N], Ff [N][nq], Fg [N][ns], E [nq][N], M [N][N], K [N][N], X [N][N]
+  std::vector<int64_t> c_rp, ff_rp, fg_rp, e_rp, m_rp, s_rp, x_rp;
+  std::vector<uint32_t> c_ci, ff_ci, fg_ci, e_ci, m_ci, s_ci, x_ci;
+  std::vector<double> c_v, ff_v, fg_v, e_v, m_v, s_v, x_v;
   int64_t cells[3] = {0, 0, 0};
 };
 
@@ -145,20 +147,27 @@ void triplets_csr(std::vector<Trip> t, int64_t rows, std::vector<int64_t> &rp, s
   for (int64_t r = 0; r < rows; ++r) rp[(size_t)r + 1] += rp[(size_t)r];
 }
 
+// The field of S.location (INSIDE: phi < 0, OUTSIDE: phi > 0); inv = the
+// other region.  Cells of location inv are skipped, ghost-penalty faces have
+// an intersected cell and a neighbour not of location inv
+// (wave/mass.h:86-105).  S.dirichlet bit 0: interface data (II, surface
+// points, stiffness.h:205-259; normal flipped for OUTSIDE), bit 1: domain
+// data (IV, boundary faces in the region, :262-330).  S.coupled: the
+// composite interface terms of compute_rhs(BlockVector) (:420-575): the own
+// field's part into C, the partner's into X.
 void assemble1d(gdm_cut_wave_system &S, const double *ls_values) {
-  const int p = S.p, n = S.n, k = S.k, n1 = p + 1;
+  const int p = S.p, n = S.n, k = S.k, n1 = p + 1, loc_f = S.location, inv = -loc_f;
   const int64_t N = n + 1;
   const double h = S.h;
   std::vector<double> gx, gw;
   gauss_unit(n1, gx, gw);
   const std::vector<double> gl = gauss_lobatto(k + 1);
   S.loc.assign(n, OUTSIDE);
-  // per cell: inside quadrature (reference s, reference weight) and surface (s, normal)
+  // per cell: the region's quadrature (reference s, reference weight) and the surface (s, level-set normal)
   std::vector<std::vector<std::pair<double, double>>> cq(n), cs(n);
   for (int c = 0; c < n; ++c) {
     const double *vals = ls_values + (size_t)c * (k + 1);
     const int where = bernstein_location(1, k, vals, gl);
-    const bool neg = where == INSIDE, pos = where == OUTSIDE;
     auto phi = [&](double s) {
       double r = 0.0;
       for (int a = 0; a <= k; ++a) {
@@ -169,13 +178,12 @@ void assemble1d(gdm_cut_wave_system &S, const double *ls_values) {
       }
       return r;
     };
-    if (neg) {
-      S.loc[c] = INSIDE;
-      for (int q = 0; q < n1; ++q) cq[c].push_back({gx[q], gw[q]});
+    S.loc[c] = (int8_t)where;
+    if (where != INTERSECTED) {
+      if (where == loc_f)
+        for (int q = 0; q < n1; ++q) cq[c].push_back({gx[q], gw[q]});
       continue;
     }
-    if (pos) continue;
-    S.loc[c] = INTERSECTED;
     constexpr int G = 64;
     double pv[G + 1];
     for (int a = 0; a <= G; ++a) pv[a] = phi((double)a / G);
@@ -206,7 +214,7 @@ void assemble1d(gdm_cut_wave_system &S, const double *ls_values) {
     pts.push_back(1.0);
     for (size_t a = 0; a + 1 < pts.size(); ++a) {
       const double s0 = pts[a], s1 = pts[a + 1];
-      if (phi(0.5 * (s0 + s1)) < 0.0)
+      if ((phi(0.5 * (s0 + s1)) < 0.0) == (loc_f == INSIDE))
         for (int q = 0; q < n1; ++q) cq[c].push_back({s0 + (s1 - s0) * gx[q], (s1 - s0) * gw[q]});
     }
     for (double r : roots) {
@@ -220,18 +228,37 @@ void assemble1d(gdm_cut_wave_system &S, const double *ls_values) {
   auto off_of = [&](int c) { return (int64_t)box_offset((unsigned)c, (unsigned)p, (unsigned)n); };
   std::vector<uint8_t> full_row((size_t)N, 0);
   for (int c = 0; c < n; ++c)
-    if (S.loc[c] != INSIDE)
+    if (S.loc[c] != loc_f)
       for (int i = 0; i < n1; ++i) full_row[(size_t)(off_of(c) + i)] = 1;
   for (int64_t r = 0; r < N; ++r)
     if (full_row[(size_t)r]) S.zero_rows.push_back(r);
-  Slots C, M, K;
+  Slots C, M, K, X;
   C.init(1, N, p + 1);
   M.init(1, N, p + 1);
   K.init(1, N, p + 1);
+  X.init(1, N, p + 1);
   std::vector<Trip> ff, fg, ev;
   Shapes sh{};
+  const double gd = S.nitsche / h, tau = 0.5 * S.nitsche / h;
+  // Nitsche terms of one Dirichlet point (normal nrm): into C (impl part, minus), K, and data column di
+  auto dirichlet_point = [&](int c, double s, double nrm, double xg) {
+    shapes_1d(p, cat_of(c), s, sh);
+    const int64_t off = off_of(c), di = (int64_t)S.sx.size();
+    S.sx.push_back(xg);
+    S.sn.push_back(nrm);
+    for (int i = 0; i < n1; ++i) {
+      const double vi = sh.v[i], gi = sh.d[i] / h;
+      fg.push_back({off + i, di, gd * vi - nrm * gi});
+      for (int j = 0; j < n1; ++j) {
+        const double vj = sh.v[j], gj = sh.d[j] / h;
+        const double a = -nrm * gi * vj - nrm * vi * gj + gd * vi * vj;
+        C.add(off + i, off + j, -a);
+        K.add(off + i, off + j, a);
+      }
+    }
+  };
   for (int c = 0; c < n; ++c) {
-    if (S.loc[c] == OUTSIDE) continue;
+    if (S.loc[c] == inv) continue;
     const int cat = cat_of(c);
     const int64_t off = off_of(c);
     const double x0 = S.lo + c * h;
@@ -253,34 +280,45 @@ void assemble1d(gdm_cut_wave_system &S, const double *ls_values) {
         }
       }
     }
-    for (const auto &sp : cs[c]) {
-      shapes_1d(p, cat, sp.first, sh);
-      const double nrm = sp.second, gd = S.nitsche / h;
-      const int64_t si = (int64_t)S.sx.size();
-      S.sx.push_back(x0 + sp.first * h);
-      S.sn.push_back(nrm);
-      for (int i = 0; i < n1; ++i) {
-        const double vi = sh.v[i], gi = sh.d[i] / h;
-        fg.push_back({off + i, si, gd * vi - nrm * gi});
-        for (int j = 0; j < n1; ++j) {
-          const double vj = sh.v[j], gj = sh.d[j] / h;
-          const double a = -nrm * gi * vj - nrm * vi * gj + gd * vi * vj;
-          C.add(off + i, off + j, -a);
-          K.add(off + i, off + j, a);
-        }
+    if (S.dirichlet & 1)
+      for (const auto &sp : cs[c]) dirichlet_point(c, sp.first, loc_f == INSIDE ? sp.second : -sp.second, x0 + sp.first * h);
+    if (S.dirichlet & 2) {
+      // boundary faces whose point lies in the region (the level set's sign there)
+      if (c == 0 && ((ls_values[0] < 0.0) == (loc_f == INSIDE)) && ls_values[0] != 0.0)
+        dirichlet_point(c, 0.0, -1.0, S.lo);
+      if (c == n - 1) {
+        const double v1 = ls_values[(size_t)c * (k + 1) + k];
+        if ((v1 < 0.0) == (loc_f == INSIDE) && v1 != 0.0) dirichlet_point(c, 1.0, 1.0, S.lo + n * h);
       }
     }
+    if (S.coupled && S.loc[c] == INTERSECTED)
+      for (const auto &sp : cs[c]) {
+        // r_own -= (-0.5 n v' [u] -+ v n {u'} +- tau v [u]), [u] = u_in - u_out, {u'} = (u_in' + u_out') / 2
+        shapes_1d(p, cat, sp.first, sh);
+        const double nr = sp.second, sg = loc_f == INSIDE ? 1.0 : -1.0;
+        for (int i = 0; i < n1; ++i) {
+          const double vi = sh.v[i], gi = sh.d[i] / h;
+          for (int j = 0; j < n1; ++j) {
+            const double vj = sh.v[j], gj = sh.d[j] / h;
+            // coefficients of u_in_j and u_out_j in the bracket
+            const double a_in = -0.5 * nr * gi * vj - sg * 0.5 * nr * vi * gj + sg * tau * vi * vj;
+            const double a_out = 0.5 * nr * gi * vj - sg * 0.5 * nr * vi * gj - sg * tau * vi * vj;
+            C.add(off + i, off + j, -(loc_f == INSIDE ? a_in : a_out));
+            X.add(off + i, off + j, -(loc_f == INSIDE ? a_out : a_in));
+          }
+        }
+      }
   }
   // ghost penalty faces (mass.h:86-105, stiffness.h:80-98): every face of a
-  // non-outside cell to a neighbour where one of the two is intersected and
-  // the other not outside, visited from both cells
+  // cell not of location inv to a neighbour where one of the two is
+  // intersected and the other not of location inv, visited from both cells
   for (int c = 0; c < n; ++c) {
-    if (S.loc[c] == OUTSIDE) continue;
+    if (S.loc[c] == inv) continue;
     for (int f = 0; f < 2; ++f) {
       const int nb = f == 0 ? c - 1 : c + 1;
       if (nb < 0 || nb >= n) continue;
       const int ln = S.loc[nb];
-      if (!((S.loc[c] == INTERSECTED && ln != OUTSIDE) || (ln == INTERSECTED && S.loc[c] != OUTSIDE))) continue;
+      if (!((S.loc[c] == INTERSECTED && ln != inv) || (ln == INTERSECTED && S.loc[c] != inv))) continue;
       // [dphi/dx] at the face: from cell c minus from the neighbour, per global DoF
       std::map<int64_t, double> jump;
       const double sc = (double)f, sn = 1.0 - f;  // face point in c's / the neighbour's reference coordinate
@@ -299,6 +337,7 @@ void assemble1d(gdm_cut_wave_system &S, const double *ls_values) {
   C.csr(S.c_rp, S.c_ci, S.c_v, false);
   M.csr(S.m_rp, S.m_ci, S.m_v, true);
   K.csr(S.s_rp, S.s_ci, S.s_v, true);
+  X.csr(S.x_rp, S.x_ci, S.x_v, false);
   triplets_csr(ff, N, S.ff_rp, S.ff_ci, S.ff_v);
   triplets_csr(fg, N, S.fg_rp, S.fg_ci, S.fg_v);
   triplets_csr(ev, (int64_t)S.qx.size(), S.e_rp, S.e_ci, S.e_v);
@@ -462,6 +501,7 @@ void assemble2d(gdm_cut_wave_system &S, const double *ls_values) {
   triplets_csr(ff, NN, S.ff_rp, S.ff_ci, S.ff_v);
   triplets_csr(fg, NN, S.fg_rp, S.fg_ci, S.fg_v);
   triplets_csr(ev, (int64_t)S.qw.size(), S.e_rp, S.e_ci, S.e_v);
+  S.x_rp.assign((size_t)NN + 1, 0);  // no coupling in 2D
 }
 
 }  // namespace
@@ -474,9 +514,13 @@ int64_t gdmh_band_cholesky(int64_t n, const int64_t *rp, const uint32_t *ci, con
                            const int64_t *rp2, const uint32_t *ci2, const double *v2, std::vector<double> &lband);
 
 int gdmh_cut_wave_create(int dim, int p, int n_sub, double lo, double hi, int ls_degree, const double *ls_values,
-                         double gamma_M, double gamma_A, double nitsche, gdm_cut_wave_system **out, char *err,
-                         size_t err_len) {
+                         int location, int flags, double gamma_M, double gamma_A, double nitsche,
+                         gdm_cut_wave_system **out, char *err, size_t err_len) {
   try {
+    if ((location != INSIDE && location != OUTSIDE) || (flags & ~7))
+      throw std::invalid_argument("cut_wave: location must be -1 (inside) or 1 (outside), flags in bits 0-2");
+    if (dim == 2 && (location != INSIDE || flags != 1))
+      throw std::invalid_argument("cut_wave: dim 2 supports the inside field with interface data only");
     if (!out || !ls_values || (dim != 1 && dim != 2) || p < 1 || p > 9 || p % 2 == 0 || n_sub < p || !(hi > lo) ||
         ls_degree < 1 || ls_degree > 9)
       throw std::invalid_argument(
@@ -485,6 +529,9 @@ int gdmh_cut_wave_create(int dim, int p, int n_sub, double lo, double hi, int ls
       throw std::invalid_argument("cut_wave: mesh too large for 32-bit column indices");
     auto *S = new gdm_cut_wave_system();
     S->dim = dim;
+    S->location = location;
+    S->dirichlet = flags & 3;
+    S->coupled = (flags & 4) != 0;
     S->p = p;
     S->n = n_sub;
     S->k = ls_degree;
@@ -518,7 +565,7 @@ void gdmh_cut_wave_info(const gdm_cut_wave_system *S, int64_t *n_dofs, int64_t *
   for (int q = 0; q < 3; ++q) cells[q] = S->cells[q];
 }
 
-// which: 0 C, 1 Ff, 2 Fg, 3 E, 4 M, 5 S (heat-impl stiffness)
+// which: 0 C, 1 Ff, 2 Fg, 3 E, 4 M, 5 K (stiffness matrix), 6 X (coupling to the partner field)
 void gdmh_cut_wave_csr(const gdm_cut_wave_system *S, int which, const int64_t **rp, const uint32_t **ci,
                        const double **v) {
   switch (which) {
@@ -527,7 +574,8 @@ void gdmh_cut_wave_csr(const gdm_cut_wave_system *S, int which, const int64_t **
     case 2: *rp = S->fg_rp.data(); *ci = S->fg_ci.data(); *v = S->fg_v.data(); return;
     case 3: *rp = S->e_rp.data(); *ci = S->e_ci.data(); *v = S->e_v.data(); return;
     case 4: *rp = S->m_rp.data(); *ci = S->m_ci.data(); *v = S->m_v.data(); return;
-    default: *rp = S->s_rp.data(); *ci = S->s_ci.data(); *v = S->s_v.data(); return;
+    case 5: *rp = S->s_rp.data(); *ci = S->s_ci.data(); *v = S->s_v.data(); return;
+    default: *rp = S->x_rp.data(); *ci = S->x_ci.data(); *v = S->x_v.data(); return;
   }
 }
 

@@ -176,11 +176,12 @@ def load():
         "gdm_cut_advection_compute_rhs": [P, P, P, P],
         "gdm_cut_advection_mass_solve": [P, P, P],
         "gdm_cut_advection_destroy": [P],
-        "gdm_cut_wave_create": [i32, i32, i32, d, d, i32, P, d, d, d, i32, ctypes.POINTER(P)],
+        "gdm_cut_wave_create": [i32, i32, i32, d, d, i32, P, i32, i32, d, d, d, i32, ctypes.POINTER(P)],
         "gdm_cut_wave_info": [P, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64), P],
         "gdm_cut_wave_points": [P, P, P, P, P],
         "gdm_cut_wave_op": [P, ctypes.POINTER(P)],
         "gdm_cut_wave_compute_rhs": [P, P, P, P, P],
+        "gdm_cut_wave_couple": [P, P, P],
         "gdm_cut_wave_mass_apply": [P, P, P],
         "gdm_cut_wave_mass_solve": [P, P, P],
         "gdm_cut_wave_system_solve": [P, d, P, P],

@@ -65,8 +65,11 @@ class CutWave:
     FE_Q(ls_degree) interpolant (values at each cell's Gauss-Lobatto points)
     defines inside (< 0)."""
 
+    INSIDE, OUTSIDE = -1, 1
+    INTERFACE_DATA, DOMAIN_DATA, COUPLED = 1, 2, 4
+
     def __init__(self, fe_degree, n_subdivisions, left, right, level_set, ls_degree=None, ghost_parameter_M=0.5,
-                 ghost_parameter_A=0.5, nitsche=None, device=0, dim=1):
+                 ghost_parameter_A=0.5, nitsche=None, device=0, dim=1, location=-1, flags=1):
         self._lib = _capi.load()
         self._h = ctypes.c_void_p()
         if dim not in (1, 2):
@@ -85,8 +88,8 @@ class CutWave:
         ls = np.ascontiguousarray(np.asarray(ls, dtype=np.float64))
         gamma_D = 5.0 * fe_degree if nitsche is None else nitsche
         check(self._lib.gdm_cut_wave_create(int(dim), int(fe_degree), int(n_subdivisions), float(left), float(right),
-                                            int(k),
-                                            ls.ctypes.data_as(ctypes.c_void_p), float(ghost_parameter_M),
+                                            int(k), ls.ctypes.data_as(ctypes.c_void_p), int(location), int(flags),
+                                            float(ghost_parameter_M),
                                             float(ghost_parameter_A), float(gamma_D), int(device),
                                             ctypes.byref(self._h)), "gdm_cut_wave_create")
         nd, nq, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
@@ -141,6 +144,11 @@ class CutWave:
                                                  _ptr(fq) if fq is not None and self.n_quad else None,
                                                  _ptr(gs) if gs is not None and self.n_surface else None, _ptr(out)),
               "gdm_cut_wave_compute_rhs")
+        return out
+
+    def couple(self, u_other, out):
+        """out += the partner field's part of the composite interface terms"""
+        check(self._lib.gdm_cut_wave_couple(self._h, _ptr(u_other), _ptr(out)), "gdm_cut_wave_couple")
         return out
 
     def mass_apply(self, u, out):
@@ -205,11 +213,15 @@ def preset(name, dim=1):
         cfl, cfl_pow = (0.3 / 9.0, 2.0) if name == "heat-rk" else (0.3, 1.0)
         return dict(base, gamma_M=0.75, gamma_A=1.5, f=f, g=ex, exact=ex, start_t=0.0, end_t=0.1, cfl=cfl,
                     cfl_pow=cfl_pow)
+    if name in ("heat-composite", "wave-composite") and dim == 1:
+        P = preset("heat-rk" if name == "heat-composite" else "wave", 1)
+        return dict(P, simulation=name, g_domain=P["g"], g=None)
     if name == "step85" and dim == 2:
         ex = lambda x, y, t: 1.0 - (x * x + y * y - 1.0)  # noqa: E731  1 - 2/dim (|x|^2 - 1)
         return dict(base, simulation="poisson", gamma_M=-1.0, gamma_A=0.5, f=lambda x, y, t: np.full_like(x, 4.0),
                     g=lambda x, y, t: np.ones_like(x), exact=ex, start_t=0.0, end_t=0.1, cfl=0.3, cfl_pow=1.0)
-    raise GdmError("cut_wave.preset: %r at dim %d (wave, heat-rk, heat-impl; step85 at dim 2)" % (name, dim))
+    raise GdmError("cut_wave.preset: %r at dim %d (wave, heat-rk, heat-impl; heat-composite, wave-composite at "
+                   "dim 1; step85 at dim 2)" % (name, dim))
 
 
 class CutWaveProblem:
@@ -321,6 +333,84 @@ class CutWaveProblem:
             self.step(t0, h)
             n += 1
             rows.append((n, t0 + h) + self.postprocess(t0 + h))
+            time.advance()
+        cw.synchronize()
+        return rows
+
+
+class CutWaveCompositeProblem:
+    """WaveProblem<1>::run for the composite presets (wave/problem.h:128-214
+    heat-rk, :346-433 wave-rk): an inside and an outside field, one CutWave
+    handle each (domain Dirichlet data + interface coupling), RK4 over the
+    blocks (u_in, u_out) or (u_in, u_out, v_in, v_out) on the device; the
+    postprocess rows alternate inside / outside."""
+
+    def __init__(self, params, device=0):
+        import torch
+
+        P = dict(params)
+        self.P, self._torch = P, torch
+        flags = CutWave.DOMAIN_DATA | CutWave.COUPLED
+        self.f = [CutWave(P["p"], P["n"], P["left"], P["right"], P["level_set"], ghost_parameter_M=P["gamma_M"],
+                          ghost_parameter_A=P["gamma_A"], nitsche=P["nitsche"], device=device, location=loc,
+                          flags=flags) for loc in (CutWave.INSIDE, CutWave.OUTSIDE)]
+        self.wave = P["simulation"] == "wave-composite"
+        self._fq = [cw.new_vector(max(cw.n_quad, 1)) for cw in self.f]
+        self._gd = [cw.new_vector(max(cw.n_surface, 1)) for cw in self.f]
+        self._vals = [cw.new_vector(max(cw.n_quad, 1)) for cw in self.f]
+
+    def _upload(self, values, dst):
+        dst[:len(values)].copy_(self._torch.from_numpy(np.ascontiguousarray(values, dtype=np.float64)))
+
+    def _accel(self, t, u0, u1):
+        """M_L^-1 (compute_rhs_L(u_L) + coupling(u_other)) for both fields"""
+        P, out = self.P, []
+        for i, (cw, u, uo) in enumerate(((self.f[0], u0, u1), (self.f[1], u1, u0))):
+            fq = gd = None
+            if P["f"] is not None and cw.n_quad:
+                self._upload(call(P["f"], cw.qx, t), self._fq[i])
+                fq = self._fq[i]
+            if cw.n_surface:
+                self._upload(call(P["g_domain"], cw.sx, t), self._gd[i])
+                gd = self._gd[i]
+            r = cw.new_vector()
+            cw.compute_rhs(u, fq, gd, r)
+            cw.couple(uo, r)
+            cw.mass_solve(r, r)
+            out.append(r)
+        return out
+
+    def _f(self, t, y):
+        if self.wave:
+            return [y[2], y[3]] + self._accel(t, y[0], y[1])
+        return self._accel(t, y[0], y[1])
+
+    def postprocess(self, t, u, i):
+        cw = self.f[i]
+        cw.eval_quadrature(u, self._vals[i])
+        e = self._vals[i][:cw.n_quad].cpu().numpy() - call(self.P["exact"], cw.qx, t)
+        return (math.sqrt(float(np.sum(e * e * cw.qw))), float(np.sum(np.abs(e) * cw.qw)),
+                float(np.max(np.abs(e))) if len(e) else 0.0)
+
+    def run(self, max_steps=None):
+        P, cw = self.P, self.f[0]
+        u = cw.new_vector()
+        self._upload(call(P["exact"], cw.vertices, P["start_t"]), u)
+        y = [u, u.clone()] + ([cw.new_vector(), cw.new_vector()] if self.wave else [])
+        dt = P["cfl"] * cw.h ** P["cfl_pow"]
+        time = DiscreteTime(P["start_t"], P["end_t"], dt)
+        rows = [(0, 0.0) + self.postprocess(0.0, y[0], 0), (0, 0.0) + self.postprocess(0.0, y[1], 1)]
+        n = 0
+        while not time.is_at_end() and (max_steps is None or n < max_steps):
+            t0, h = time.t, time.next_step_size()
+            # TimeStepping::ExplicitRungeKutta, RK_CLASSIC_FOURTH_ORDER
+            ks = []
+            for s in range(4):
+                ys = y if s == 0 else [yb + (h * RK4_A[s - 1]) * kb for yb, kb in zip(y, ks[-1])]
+                ks.append(self._f(t0 + RK4_C[s] * h, ys))
+            y = [yb + sum((h * RK4_B[s]) * ks[s][b] for s in range(4)) for b, yb in enumerate(y)]
+            n += 1
+            rows += [(n, t0 + h) + self.postprocess(t0 + h, y[0], 0), (n, t0 + h) + self.postprocess(t0 + h, y[1], 1)]
             time.advance()
         cw.synchronize()
         return rows

@@ -502,17 +502,35 @@ int gdm_cut_advection_destroy(gdm_cut_advection *c);
  * QuadratureGenerator (Saye) on the cell polynomial.  DoFs: vertices,
  * lexicographic (x fastest).  Vectors: device pointers (n_dofs, n_quad,
  * n_surface doubles).
+ *
+ * Composite presets (heat-composite, wave-composite; dim 1): one handle per
+ * field, location GDM_CUT_INSIDE (phi < 0) or GDM_CUT_OUTSIDE (phi > 0), each
+ * with its region's quadrature, mass and ghost-penalty faces (an intersected
+ * cell and a neighbour not of the other location); flags select the Nitsche
+ * data: GDM_CUT_WAVE_INTERFACE_DATA (II, the surface points; the presets
+ * without composite), GDM_CUT_WAVE_DOMAIN_DATA (IV, the domain boundary faces
+ * in the region, stiffness.h:262-330) and GDM_CUT_WAVE_COUPLED (the interface
+ * terms of compute_rhs(BlockVector), stiffness.h:420-575: the own field's
+ * part in compute_rhs, the partner's added by gdm_cut_wave_couple(c,
+ * u_partner, rhs)).  The data points of gdm_cut_wave_points (sx, sn) are the
+ * interface points followed by the domain faces, as selected.
  * ------------------------------------------------------------------------ */
 typedef struct gdm_cut_wave gdm_cut_wave;
+#define GDM_CUT_INSIDE (-1)
+#define GDM_CUT_OUTSIDE 1
+#define GDM_CUT_WAVE_INTERFACE_DATA 1
+#define GDM_CUT_WAVE_DOMAIN_DATA 2
+#define GDM_CUT_WAVE_COUPLED 4
 int gdm_cut_wave_create(int dim, int fe_degree, int n_subdivisions, double left, double right, int ls_degree,
-                        const double *ls_values, double gamma_M, double gamma_A, double nitsche, int device,
-                        gdm_cut_wave **out);
+                        const double *ls_values, int location, int flags, double gamma_M, double gamma_A,
+                        double nitsche, int device, gdm_cut_wave **out);
 /* cells[3] = inside, intersected, outside */
 int gdm_cut_wave_info(const gdm_cut_wave *c, int64_t *n_dofs, int64_t *n_quad, int64_t *n_surface, int64_t *cells);
 /* host arrays: quadrature points [n_quad][dim] and JxW [n_quad], surface points and unit normals [n_surface][dim] */
 int gdm_cut_wave_points(const gdm_cut_wave *c, double *qx, double *qw, double *sx, double *sn);
 int gdm_cut_wave_op(gdm_cut_wave *c, gdm_op **op);
 int gdm_cut_wave_compute_rhs(gdm_cut_wave *c, const double *u, const double *fq, const double *gs, double *rhs);
+int gdm_cut_wave_couple(gdm_cut_wave *c, const double *u_other, double *rhs);
 int gdm_cut_wave_mass_apply(gdm_cut_wave *c, const double *u, double *out);
 int gdm_cut_wave_mass_solve(gdm_cut_wave *c, const double *rhs, double *x);
 int gdm_cut_wave_system_solve(gdm_cut_wave *c, double dt, const double *rhs, double *x);

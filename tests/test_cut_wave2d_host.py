@@ -50,7 +50,7 @@ def host_system2d(prm):
     ls = np.ascontiguousarray(np.hypot(X, Y).reshape(-1) - 1.0)
     S = ctypes.c_void_p()
     err = ctypes.create_string_buffer(256)
-    assert L.gdmh_cut_wave_create(2, p, n, left, right, p, ls.ctypes.data, prm["gamma_M"], prm["gamma_A"],
+    assert L.gdmh_cut_wave_create(2, p, n, left, right, p, ls.ctypes.data, -1, 1, prm["gamma_M"], prm["gamma_A"],
                                   prm["nitsche"], ctypes.byref(S), err, 256) == 0, err.value
     try:
         nd, nq, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

@@ -34,7 +34,8 @@ def _lib():
 
     L = gdm_amd.load()
     P, I64, D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_double
-    L.gdmh_cut_wave_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, D, D, ctypes.c_int, P, D, D, D,
+    L.gdmh_cut_wave_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, D, D, ctypes.c_int, P,
+                                       ctypes.c_int, ctypes.c_int, D, D, D,
                                        ctypes.POINTER(P), ctypes.c_char_p, ctypes.c_size_t]
     L.gdmh_cut_wave_info.argtypes = [P] + [ctypes.POINTER(I64)] * 3 + [P]
     L.gdmh_cut_wave_csr.argtypes = [P, ctypes.c_int] + [ctypes.POINTER(ctypes.c_void_p)] * 3
@@ -47,8 +48,9 @@ def _arr(ptr, n, dt):
     return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(dt)), shape=(n,)).copy() if n else np.zeros(0)
 
 
-def host_system(prm):
-    """dict of the device operator's host arrays (dense matrices) for a preset"""
+def host_system(prm, location=-1, flags=1):
+    """dict of the device operator's host arrays (dense matrices) for a preset
+    (the field of `location`, Nitsche data / coupling `flags`)"""
     import gdm_amd.cut_wave as CW
 
     L = _lib()
@@ -59,16 +61,16 @@ def host_system(prm):
     ls = np.ascontiguousarray((np.abs(x) - 1.0).reshape(-1))
     S = ctypes.c_void_p()
     err = ctypes.create_string_buffer(256)
-    assert L.gdmh_cut_wave_create(1, p, n, left, right, p, ls.ctypes.data, prm["gamma_M"], prm["gamma_A"],
+    assert L.gdmh_cut_wave_create(1, p, n, left, right, p, ls.ctypes.data, location, flags, prm["gamma_M"], prm["gamma_A"],
                                   prm["nitsche"], ctypes.byref(S), err, 256) == 0, err.value
     try:
         nd, nq, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         cells = (ctypes.c_int64 * 3)()
         L.gdmh_cut_wave_info(S, ctypes.byref(nd), ctypes.byref(nq), ctypes.byref(ns), cells)
         N, NQ, NS = nd.value, nq.value, ns.value
-        shape = {0: (N, N), 1: (N, NQ), 2: (N, NS), 3: (NQ, N), 4: (N, N), 5: (N, N)}
+        shape = {0: (N, N), 1: (N, NQ), 2: (N, NS), 3: (NQ, N), 4: (N, N), 5: (N, N), 6: (N, N)}
         out = {}
-        for w, name in enumerate(("C", "Ff", "Fg", "E", "M", "K")):
+        for w, name in enumerate(("C", "Ff", "Fg", "E", "M", "K", "X")):
             q = [ctypes.c_void_p() for _ in range(3)]
             L.gdmh_cut_wave_csr(S, w, *[ctypes.byref(x) for x in q])
             rows, cols = shape[w]
@@ -176,6 +178,70 @@ def test_device_formulation_reproduces_golden(case, simulation):
             u = np.linalg.solve(H["M"] + dt * H["K"], H["M"] @ u + dt * rhs(u, t0 + dt, False))
         n += 1
         rows.append((n, t0 + dt) + post(u, t0 + dt))
+        time.advance()
+    ref = REF[case]["steps"]
+    assert len(rows) == len(ref)
+    for got, exp in zip(rows, ref):
+        assert got[0] == exp[0] and abs(got[1] - exp[1]) <= 5.000001e-6
+        np.testing.assert_allclose(got[2:], exp[2:], rtol=2e-8, atol=0)
+
+
+@pytest.mark.parametrize("case,simulation", [("wave_composite_0", "wave-composite"),
+                                             ("heat_composite_0", "heat-composite")])
+def test_composite_device_formulation(case, simulation):
+    """the composite presets with the device operators of two handles
+    (inside: domain data + coupling, outside: domain data + coupling):
+    r_own = (Z S + C) u_own + X u_other + Ff f + Fg g_D; the matrices against
+    the oracle's, the time loop against the goldens"""
+    P = cut1d.composite_params(simulation)
+    flags = 2 | 4
+    H = [host_system(P, loc, flags) for loc in (-1, 1)]
+    m = cut1d.Cut1D(P["p"], P["n"], P["left"], P["right"], cut1d._sphere)
+    N = m.N
+    for h, loc in zip(H, (-1, 1)):
+        M = m.mass_matrix(P["gamma_M"], loc)
+        np.testing.assert_allclose(h["M"], M, rtol=0, atol=1e-13 * abs(M).max())
+    # the operator parts, column by column: own field and partner
+    for e in np.eye(N)[:: 3]:
+        c0, c1 = m.coupling(e, np.zeros(N), P["nitsche"])
+        d0, d1 = m.coupling(np.zeros(N), e, P["nitsche"])
+        zero = lambda x, t: 0.0  # noqa: E731
+        own0 = m.rhs(e, 0.0, True, P["gamma_A"], P["nitsche"], location=-1, g_domain=zero) + c0
+        own1 = m.rhs(e, 0.0, True, P["gamma_A"], P["nitsche"], location=1, g_domain=zero) + d1
+        for got, ref in ((H[0]["A"] @ e, own0), (H[1]["A"] @ e, own1), (H[0]["X"] @ e, d0), (H[1]["X"] @ e, c1)):
+            np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12 * max(abs(ref).max(), 1.0))
+    Minv = [np.linalg.inv(h["M"]) for h in H]
+    h_ = (P["right"] - P["left"]) / P["n"]
+
+    def data(h, t):
+        r = h["Ff"] @ np.array([P["f"](x, t) for x in h["qx"]]) if P["f"] else np.zeros(N)
+        return r + h["Fg"] @ np.array([P["g_domain"](x, t) for x in h["sx"]])
+
+    def fields(t, u0, u1):
+        r0 = H[0]["A"] @ u0 + H[0]["X"] @ u1 + data(H[0], t)
+        r1 = H[1]["A"] @ u1 + H[1]["X"] @ u0 + data(H[1], t)
+        return Minv[0] @ r0, Minv[1] @ r1
+
+    def post(h, u, t):
+        e = h["E"] @ u - np.array([P["exact"](x, t) for x in h["qx"]])
+        return np.sqrt(np.sum(e * e * h["qw"])), np.sum(np.abs(e) * h["qw"]), np.max(np.abs(e))
+
+    xv = P["left"] + np.arange(N) * h_
+    u = np.array([P["exact"](x, P["start_t"]) for x in xv])
+    if simulation == "wave-composite":
+        y = np.concatenate([u, u, np.zeros(2 * N)])
+        f = lambda t, y: np.concatenate([y[2 * N:], *fields(t, y[:N], y[N:2 * N])])  # noqa: E731
+    else:
+        y = np.concatenate([u, u])
+        f = lambda t, y: np.concatenate(fields(t, y[:N], y[N:]))  # noqa: E731
+    time = cut1d.DiscreteTime(P["start_t"], P["end_t"], P["cfl"] * h_ ** P["cfl_pow"])
+    rows = [(0, 0.0) + post(H[0], u, 0.0), (0, 0.0) + post(H[1], u, 0.0)]
+    n = 0
+    while not time.is_at_end():
+        t0, dt = time.t, time.next_step_size()
+        y = cut1d.rk4_step(f, t0, dt, y)
+        n += 1
+        rows += [(n, t0 + dt) + post(H[0], y[:N], t0 + dt), (n, t0 + dt) + post(H[1], y[N:2 * N], t0 + dt)]
         time.advance()
     ref = REF[case]["steps"]
     assert len(rows) == len(ref)

@@ -1,7 +1,7 @@
 # consumer-wave priority A/B (s_setprio in the stencil consumer waves): C3 p=5 and C4 p=7
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r3p; mkdir -p $OUT
+OUT=${OUT:-gpurun_out/r3p}; mkdir -p $OUT
 L=$PWD/dealii-galerkin-difference-methods_amd/lib/variants
 run() {  # name lib p kind config
   local name=$1 lib=$2 p=$3 kind=$4 cfg=$5
