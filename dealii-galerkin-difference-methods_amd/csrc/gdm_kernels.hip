@@ -1098,10 +1098,6 @@ __device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) 
   using G = Geom8<P, R, NC, NP, BK>;
   const int ybase = t.y0 + (t.wv - NP) * R;
   const bool full = (t.x0 + G::TX <= a.Nx) && (ybase + R <= a.out_y1);
-#ifdef GDM_CONS_PRIO
-  // experiment: consumer waves (the per-plane critical path) issue first
-  __builtin_amdgcn_s_setprio(GDM_CONS_PRIO);
-#endif
   // edge tiles (rows next to a y wall) wait for the producers' y-wall
   // corrections every plane: their own copy of the loop keeps that out of the
   // hot block of the other tiles
