@@ -27,25 +27,32 @@ RK4_B = (1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0)
 
 
 class DiscreteTime:
-    """deal.II DiscreteTime: fixed steps; the last one shrunk to hit the end
-    time, or the previous one stretched when the remainder is below 5 %."""
+    """deal.II DiscreteTime (base/discrete_time.cc): the next time is the
+    current one plus the last step, the step recomputed as the difference of
+    the two times (round-off accumulates as in the reference), snapped to the
+    end time when within 5 % of a step of it."""
 
     def __init__(self, start, end, dt):
-        self.t, self.end, self.dt, self.step = float(start), float(end), float(dt), 0
+        self.t, self.end, self.step = float(start), float(end), 0
+        self._next = self._next_time(self.t, float(dt))
+
+    def _next_time(self, current, step):
+        n = current + step
+        if step > 0.0 and n > self.end - 0.05 * step:
+            n = self.end
+        return n
 
     def is_at_end(self):
-        return not (self.t < self.end)
+        return self.t == self.end
 
     def next_step_size(self):
-        if self.t + self.dt + 0.05 * self.dt > self.end:
-            return self.end - self.t
-        return self.dt
+        return self._next - self.t
 
     def advance(self):
-        h = self.next_step_size()
-        self.t = self.end if self.t + h >= self.end else self.t + h
+        step = self._next - self.t
+        self.t = self._next
+        self._next = self._next_time(self.t, step)
         self.step += 1
-
 
 class WaveProblem:
     """wave-rk on one rank: du/dt = v, dv/dt = M^-1 (K u) with K the wave

@@ -425,26 +425,31 @@ class MassMatrixOperator {
   mutable int sp_rounds = -1;                                 // solve_spike refinement rounds (cached)
 };
 
-// deal.II DiscreteTime: fixed steps, the last one shrunk to hit end_t or, when
-// the remainder would be tiny, the previous one stretched.
+// deal.II DiscreteTime (base/discrete_time.cc): the next time is the current
+// one plus the last step, the step itself recomputed as the difference of the
+// two times (so round-off accumulates exactly as in the reference), snapped to
+// the end time when within 5 % of a step of it.
 class DiscreteTime {
  public:
-  DiscreteTime(double start, double end, double dt) : t(start), end(end), dt(dt) {}
-  bool is_at_end() const { return !(t < end); }
+  DiscreteTime(double start, double end, double dt) : t(start), end(end), next(next_time(start, dt, end)) {}
+  bool is_at_end() const { return t == end; }
   double get_current_time() const { return t; }
-  double get_next_step_size() const {
-    if (t + dt >= end || t + 1.05 * dt > end) return end - t;
-    return dt;
-  }
+  double get_next_step_size() const { return next - t; }
   void advance_time() {
-    const double h = get_next_step_size();
-    t = (t + h >= end) ? end : t + h;
+    const double step = next - t;
+    t = next;
+    next = next_time(t, step, end);
     ++steps;
   }
   unsigned int get_step_number() const { return steps; }
 
  private:
-  double t, end, dt;
+  static double next_time(double current, double step, double end) {
+    double n = current + step;
+    if (step > 0.0 && n > end - 0.05 * step) n = end;
+    return n;
+  }
+  double t, end, next;
   unsigned int steps = 0;
 };
 

@@ -62,25 +62,32 @@ def gauss_lobatto(n):
 
 
 class DiscreteTime:
-    """deal.II DiscreteTime: fixed steps; the last one shrunk to hit end, or
-    the previous one stretched when the remainder is below 5 % of a step."""
+    """deal.II DiscreteTime (base/discrete_time.cc): the next time is the
+    current one plus the last step, the step recomputed as the difference of
+    the two times (round-off accumulates as in the reference), snapped to the
+    end time when within 5 % of a step of it."""
 
     def __init__(self, start, end, dt):
-        self.t, self.end, self.dt, self.step = start, end, dt, 0
+        self.t, self.end, self.step = float(start), float(end), 0
+        self._next = self._next_time(self.t, float(dt))
+
+    def _next_time(self, current, step):
+        n = current + step
+        if step > 0.0 and n > self.end - 0.05 * step:
+            n = self.end
+        return n
 
     def is_at_end(self):
-        return not (self.t < self.end)
+        return self.t == self.end
 
     def next_step_size(self):
-        if self.t + self.dt + 0.05 * self.dt > self.end:
-            return self.end - self.t
-        return self.dt
+        return self._next - self.t
 
     def advance(self):
-        h = self.next_step_size()
-        self.t = self.end if self.t + h >= self.end else self.t + h
+        step = self._next - self.t
+        self.t = self._next
+        self._next = self._next_time(self.t, step)
         self.step += 1
-
 
 RK4 = dict(a=[[], [0.5], [0.0, 0.5], [0.0, 0.0, 1.0]], b=[1 / 6, 1 / 3, 1 / 3, 1 / 6], c=[0.0, 0.5, 0.5, 1.0])
 
