@@ -269,7 +269,12 @@ class WaveProblem {
     const int flags = comp ? (GDM_CUT_WAVE_DOMAIN_DATA | GDM_CUT_WAVE_COUPLED) : GDM_CUT_WAVE_INTERFACE_DATA;
     std::vector<std::unique_ptr<Field<dim>>> F;
     F.emplace_back(new Field<dim>(P, GDM_CUT_INSIDE, flags, device_));
-    if (comp) F.emplace_back(new Field<dim>(P, GDM_CUT_OUTSIDE, flags, device_));
+    if (comp) {
+      F.emplace_back(new Field<dim>(P, GDM_CUT_OUTSIDE, flags, device_));
+      // both fields' operators and the block updates on one stream (the HIP null stream): the coupling reads the
+      // partner's stage vector
+      for (auto &f : F) check(gdm_op_set_stream(f->op(), nullptr), "gdm_op_set_stream");
+    }
     gdm_op *op = F[0]->op();
     const size_t N = (size_t)F[0]->n_dofs;
     const Function &dbc = comp ? P.function_domain_dbc : P.function_interface_dbc;
