@@ -310,6 +310,17 @@ struct Geo3 {
 #endif
 
 // line-end chunks: 2 = per-group table / interior-row decision, 1 = tables for the whole chunk
+// cache policy of the v3 kernels' global accesses (buffer aux bits on gfx950:
+// 2 = nt): the line data stream through once per pass, so loads and stores are
+// non-temporal.  A/B on the MI355X (profiles/r3v, mass solve): C3 1.515 ->
+// 1.425 ms, C4 0.323 -> 0.249 ms, C2 0.0378 -> 0.0356 ms; stores alone gave
+// -2 % / -1 % / -7 %, loads alone nothing
+#ifndef GDM_MASS_LD_CPOL
+#define GDM_MASS_LD_CPOL 2
+#endif
+#ifndef GDM_MASS_ST_CPOL
+#define GDM_MASS_ST_CPOL 2
+#endif
 #ifndef GDM_MASS_EDGE_MODE
 #define GDM_MASS_EDGE_MODE 1
 #endif
@@ -530,13 +541,13 @@ __global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel
     uint32_t o = min(lo, last);
     asm volatile("" : "+s"(o));
     lo += s8;
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lbyte, o, 0));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lbyte, o, GDM_MASS_LD_CPOL));
   };
   auto put = [&](double v) {
     uint32_t o = so;
     asm volatile("" : "+s"(o));
     so += s8;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rd, lbyte, o, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rd, lbyte, o, GDM_MASS_ST_CPOL);
   };
   double fifo[Q];
   auto get = [&](int j) -> double {
@@ -647,7 +658,7 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
       const int u = q * 64 + ln, row = u / UPR, pair = u - row * UPR;
       const uint32_t voff = (uint32_t)(((int64_t)row * len + base + 2 * pair) * 8);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(t + q * 64), 16,
-                                               voff, 0, 0, 0);
+                                               voff, 0, 0, GDM_MASS_LD_CPOL);
     }
   };
   // b values of the lane's row, read QL pairs ahead from the tile
@@ -683,7 +694,11 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
       const int u = q * 64 + ln;
       const int row = min(u / UPR, nl - 1), pair = min(u % UPR, last_pair);
       const dpair v = t[row * UPR + pair];
+#if GDM_MASS_ST_CPOL
+      __builtin_nontemporal_store(v, reinterpret_cast<dpair *>(dbase + (int64_t)row * len + base + 2 * pair));
+#else
       *reinterpret_cast<dpair *>(dbase + (int64_t)row * len + base + 2 * pair) = v;
+#endif
     }
     GDM_FENCE();
   };
