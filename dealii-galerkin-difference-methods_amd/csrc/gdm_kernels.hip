@@ -41,6 +41,20 @@
 #ifndef GDM_PF7
 #define GDM_PF7 3
 #endif
+// cache policy of the v8 stencil's plane DMA (buffer aux bits on gfx950: 2 =
+// nt) and its output stores (1 = non-temporal)
+#ifndef GDM_STENCIL_LD_CPOL
+#define GDM_STENCIL_LD_CPOL 0
+#endif
+#ifndef GDM_STENCIL_ST_NT
+#define GDM_STENCIL_ST_NT 0
+#endif
+#if GDM_STENCIL_ST_NT
+#define GDM_STENCIL_STORE(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define GDM_STENCIL_STORE(p, v) (*(p) = (v))
+#endif
+
 namespace gdmk {
 
 
@@ -244,9 +258,9 @@ __device__ __forceinline__ void stage_plane_pre7(const StencilArgs &a, const Til
         if (i < ni && d.vo[ps][i] != 0xffffffffu) {
           auto *dst = (__attribute__((address_space(3))) void *)(gbase + i * 64 * CH);
           if constexpr (CH == 16)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, d.vo[ps][i], 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, d.vo[ps][i], 0, 0, GDM_STENCIL_LD_CPOL);
           else
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, d.vo[ps][i], 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, d.vo[ps][i], 0, 0, GDM_STENCIL_LD_CPOL);
         }
       }
     }
@@ -1053,11 +1067,11 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
     double *orow = a.dst + ((int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) + (ybase - a.out_y0)) * Nx + x;
     if (full) {
 #pragma unroll
-      for (int j = 0; j < R; ++j) orow[(int64_t)j * Nx] = acc[rslot][j];
+      for (int j = 0; j < R; ++j) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
     } else {
 #pragma unroll
       for (int j = 0; j < R; ++j)
-        if (x < Nx && ybase + j < a.out_y1) orow[(int64_t)j * Nx] = acc[rslot][j];
+        if (x < Nx && ybase + j < a.out_y1) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
     }
   }
 #pragma unroll

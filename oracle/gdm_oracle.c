@@ -732,19 +732,6 @@ int gdmo_wave_rhs(int dim, int p, const unsigned *nsub, const double *lo, const 
 /* Returns nnz; rowptr (n+1), cols, vals preallocated by caller with           */
 /* capacity cap (call with cols == NULL to query nnz).                        */
 /* ------------------------------------------------------------------------- */
-static int64_t csr_find(const int64_t *rowptr, const int64_t *cols, int64_t r, int64_t c)
-{
-  int64_t lo = rowptr[r], hi = rowptr[r + 1];
-  while (lo < hi) {
-    const int64_t m = (lo + hi) / 2;
-    if (cols[m] < c)
-      lo = m + 1;
-    else
-      hi = m;
-  }
-  return lo;
-}
-
 int64_t gdmo_matrix_csr(int dim, int p, const unsigned *nsub, const double *lo, const double *hi,
                         int kind, int64_t *rowptr, int64_t *cols, double *vals)
 {
@@ -799,54 +786,76 @@ int64_t gdmo_matrix_csr(int dim, int p, const unsigned *nsub, const double *lo, 
   const int nd = T.nd, n1 = p + 1;
   const unsigned nc = n_cells_total(dim, nsub);
   uint64_t *dofs = (uint64_t *)malloc(sizeof(uint64_t) * nd);
-  double *sv = (double *)malloc(sizeof(double) * nd * nd);
-  double *sg = (double *)malloc(sizeof(double) * nd * nd * 3);
   double *cm = (double *)malloc(sizeof(double) * nd * nd);
-  unsigned prev_cat[3] = {~0u, ~0u, ~0u};
   for (unsigned c = 0; c < nc; ++c) {
     unsigned cidx[3], cat[3];
     double h[3];
     cell_setup(dim, p, nsub, c, lo, hi, cidx, cat, h);
-    if (cat[0] != prev_cat[0] || cat[1] != prev_cat[1] || cat[2] != prev_cat[2]) {
-      for (int i = 0; i < nd; ++i)
-        for (int q = 0; q < nd; ++q)
-          shape_at(&T, cat, i, q, h, &sv[i * nd + q], &sg[3 * (i * nd + q)]);
-      memcpy(prev_cat, cat, sizeof(cat));
-    }
-    double jxw_vol = 1.0;
+    /* the tensor-product QGauss(p+1) element matrix, sum-factorised: 1D mass
+       M_d[i][j] = h_d sum_q w_q v_i v_j and stiffness K_d[i][j] = 1 / h_d
+       sum_q w_q v_i' v_j' per direction; mass = M_z x M_y x M_x, Laplace =
+       sum_e (K_e in direction e, M elsewhere) -- the same quadrature sums as
+       the cell loop, in a different order */
+    double M1[3][MAXN][MAXN], K1[3][MAXN][MAXN];
     for (int d = 0; d < dim; ++d)
-      jxw_vol *= h[d];
-    gdmo_cell_dof_indices(dim, p, nsub, c, dofs);
-    memset(cm, 0, sizeof(double) * nd * nd);
-    for (int q = 0; q < nd; ++q) {
-      int rq = q;
-      double wq = jxw_vol;
-      for (int d = 0; d < dim; ++d) {
-        wq *= T.wq[rq % n1];
-        rq /= n1;
-      }
-      for (int i = 0; i < nd; ++i)
-        for (int j = 0; j < nd; ++j) {
-          double s;
-          if (kind == 0)
-            s = sv[i * nd + q] * sv[j * nd + q];
-          else {
-            s = 0.0;
-            for (int e = 0; e < dim; ++e)
-              s += sg[3 * (i * nd + q) + e] * sg[3 * (j * nd + q) + e];
+      for (int i = 0; i < n1; ++i)
+        for (int j = 0; j < n1; ++j) {
+          double m = 0.0, k = 0.0;
+          for (int q = 0; q < n1; ++q) {
+            m += T.wq[q] * T.v1[cat[d]][i][q] * T.v1[cat[d]][j][q];
+            k += T.wq[q] * T.g1[cat[d]][i][q] * T.g1[cat[d]][j][q];
           }
-          cm[i * nd + j] += s * wq;
+          M1[d][i][j] = m * h[d];
+          K1[d][i][j] = k / h[d];
         }
-    }
     for (int i = 0; i < nd; ++i)
       for (int j = 0; j < nd; ++j) {
-        const int64_t k = csr_find(rowptr, cols, (int64_t)dofs[i], (int64_t)dofs[j]);
+        int ii[3] = {0, 0, 0}, jj[3] = {0, 0, 0}, ri = i, rj = j;
+        for (int d = 0; d < dim; ++d) {
+          ii[d] = ri % n1;
+          ri /= n1;
+          jj[d] = rj % n1;
+          rj /= n1;
+        }
+        double s;
+        if (kind == 0) {
+          s = 1.0;
+          for (int d = 0; d < dim; ++d) s *= M1[d][ii[d]][jj[d]];
+        } else {
+          s = 0.0;
+          for (int e = 0; e < dim; ++e) {
+            double t = 1.0;
+            for (int d = 0; d < dim; ++d) t *= (d == e ? K1[d] : M1[d])[ii[d]][jj[d]];
+            s += t;
+          }
+        }
+        cm[i * nd + j] = s;
+      }
+    gdmo_cell_dof_indices(dim, p, nsub, c, dofs);
+    for (int i = 0; i < nd; ++i) {
+      /* row r's columns are its |i_d - j_d| <= p box, sorted z, y, x: the
+         position of column c is arithmetic */
+      const int64_t r = (int64_t)dofs[i];
+      int64_t id[3] = {0, 0, 0}, rem = r, lo_[3] = {0, 0, 0}, w[3] = {1, 1, 1};
+      for (int d = 0; d < dim; ++d) {
+        id[d] = rem % N[d];
+        rem /= N[d];
+        lo_[d] = id[d] - p < 0 ? 0 : id[d] - p;
+        const int64_t hi_ = id[d] + p > (int64_t)N[d] - 1 ? N[d] - 1 : id[d] + p;
+        w[d] = hi_ - lo_[d] + 1;
+      }
+      for (int j = 0; j < nd; ++j) {
+        int64_t cj = (int64_t)dofs[j], jd[3] = {0, 0, 0};
+        for (int d = 0; d < dim; ++d) {
+          jd[d] = cj % N[d];
+          cj /= N[d];
+        }
+        const int64_t k = rowptr[r] + ((jd[2] - lo_[2]) * w[1] + (jd[1] - lo_[1])) * w[0] + (jd[0] - lo_[0]);
         vals[k] += cm[i * nd + j];
       }
+    }
   }
   free(dofs);
-  free(sv);
-  free(sg);
   free(cm);
   return nnz;
 }
