@@ -42,12 +42,14 @@
 #define GDM_PF7 3
 #endif
 // cache policy of the v8 stencil's plane DMA (buffer aux bits on gfx950: 2 =
-// nt) and its output stores (1 = non-temporal)
+// nt) and its output stores (1 = non-temporal).  A/B at C3 on the MI355X
+// (profiles/r3x, 3 repetitions each): cached 0.840-0.849 ms, non-temporal
+// stores 0.822-0.837 ms (the default), non-temporal stores and DMA 0.835-0.845
 #ifndef GDM_STENCIL_LD_CPOL
 #define GDM_STENCIL_LD_CPOL 0
 #endif
 #ifndef GDM_STENCIL_ST_NT
-#define GDM_STENCIL_ST_NT 0
+#define GDM_STENCIL_ST_NT 1
 #endif
 #if GDM_STENCIL_ST_NT
 #define GDM_STENCIL_STORE(p, v) __builtin_nontemporal_store((v), (p))
