@@ -98,6 +98,8 @@ struct SpikeTables {
   bool built = false;
   double eps = 0.0;        // largest dropped far-spike entry over all slabs
   int rounds = 0;          // refinement exchanges (-1: partition refused)
+  int next_round = -1;     // progress of the current solve: -1 no slab solve
+                           // pending, k: rounds [0, k) done
   double *G0 = nullptr;    // device [2p][plane]: saved slab-solve edge planes (rounds > 0)
   int n_planes = 0;        // owned planes of this rank
   int has_lo = 0, has_hi = 0;
@@ -1484,7 +1486,9 @@ int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned) {
                   op->spike.eps, kSpikeMaxRounds, kSpikeTol);
     return fail(GDM_ERR_UNSUPPORTED, msg);
   }
+  op->spike.next_round = -1;
   mass_solve_passes(op, rhs_owned, x_owned, &op->spike.slab);
+  op->spike.next_round = 0;
   return GDM_OK;
   GDM_GUARD_END
 }
@@ -1492,11 +1496,20 @@ int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned) {
 int gdm_mass_solve_interface(gdm_op *op, double *x_local) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   if (op->mesh.n_ranks == 1) return GDM_OK;
-  if (!op->spike.built || op->spike.rounds < 0)
+  if (!op->spike.built || op->spike.rounds < 0 || op->spike.next_round < 0)
     return fail(GDM_ERR_STATE, "gdm_mass_solve_interface: call gdm_mass_solve_slab first");
+  if (op->spike.next_round != op->spike.rounds) {
+    char msg[160];
+    std::snprintf(msg, sizeof msg,
+                  "gdm_mass_solve_interface: %d of %d refinement rounds ran since gdm_mass_solve_slab "
+                  "(gdm_mass_solve_interface_round)",
+                  op->spike.next_round, op->spike.rounds);
+    return fail(GDM_ERR_STATE, msg);
+  }
   if (op->layout.n_owned > 0 && !x_local) return fail(GDM_ERR_ARG, "NULL vector");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
+  op->spike.next_round = -1;
   const SpikeTables &S = op->spike;
   if ((S.k_end > S.k_begin || S.rounds > 0) && (S.has_lo || S.has_hi))
     hip_check(gdmk_launch_spike(op->p, x_local, op->layout.plane_size,
@@ -1514,9 +1527,13 @@ int gdm_mass_solve_interface_round(gdm_op *op, double *x_local, int round) {
   if (!op->spike.built || op->spike.rounds < 0)
     return fail(GDM_ERR_STATE, "gdm_mass_solve_interface_round: call gdm_mass_solve_slab first");
   if (round < 0 || round >= op->spike.rounds) return fail(GDM_ERR_ARG, "round out of range [0, rounds)");
+  if (op->spike.next_round < 0)
+    return fail(GDM_ERR_STATE, "gdm_mass_solve_interface_round: call gdm_mass_solve_slab first");
+  if (round != op->spike.next_round) return fail(GDM_ERR_STATE, "gdm_mass_solve_interface_round: rounds run in order");
   if (op->layout.n_owned > 0 && !x_local) return fail(GDM_ERR_ARG, "NULL vector");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
+  ++op->spike.next_round;
   const SpikeTables &S = op->spike;
   hip_check(gdmk_launch_spike(op->p, x_local, op->layout.plane_size,
                               (int64_t)op->layout.ghost_planes_below * op->layout.plane_size, S.n_planes, S.has_lo,

@@ -242,6 +242,13 @@ def mass_spike_rounds(dim, fe_degree, n_subdivisions, n_ranks, lo=0.0, hi=1.0):
     return r.value
 
 
+def mesh_spike_rounds(m):
+    """mass_spike_rounds for an existing gdm_mesh_desc (an operator's .mesh)."""
+    r = ctypes.c_int(0)
+    check(load().gdm_mass_spike_rounds(ctypes.byref(m), ctypes.byref(r)), "gdm_mass_spike_rounds")
+    return r.value
+
+
 def mass_spike_eps(dim, fe_degree, n_subdivisions, n_ranks, lo=0.0, hi=1.0):
     """Largest coupling the distributed mass inverse's truncated interface
     systems drop (pure host, no GPU); the solve needs <= 1e-15."""

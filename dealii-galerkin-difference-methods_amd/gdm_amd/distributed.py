@@ -219,9 +219,15 @@ class SlabMassSolve:
 
     `op` is the rank's GdmOperator (or any object with mass_solve_slab /
     mass_solve_interface[_round] / owned_view), `halo` its HaloExchange (None on
-    one rank).  solve(rhs_owned, x_local) returns the owned view of x_local."""
+    one rank).  solve(rhs_owned, x_local) returns the owned view of x_local.
+    `rounds` None asks gdm_mass_spike_rounds for the operator's mesh (the C
+    ABI refuses an interface call whose rounds did not all run)."""
 
-    def __init__(self, op, halo, rounds=0):
+    def __init__(self, op, halo, rounds=None):
+        if rounds is None:
+            from . import _capi
+
+            rounds = _capi.mesh_spike_rounds(op.mesh)
         self.op, self.halo, self.rounds = op, halo, int(rounds)
 
     def solve(self, rhs_owned, x_local):

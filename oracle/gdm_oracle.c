@@ -786,51 +786,77 @@ int64_t gdmo_matrix_csr(int dim, int p, const unsigned *nsub, const double *lo, 
   const int nd = T.nd, n1 = p + 1;
   const unsigned nc = n_cells_total(dim, nsub);
   uint64_t *dofs = (uint64_t *)malloc(sizeof(uint64_t) * nd);
-  double *cm = (double *)malloc(sizeof(double) * nd * nd);
+  const unsigned ncat = MAXP;
+  double **cache = (double **)calloc((size_t)ncat * ncat * ncat, sizeof(double *));
+  /* element matrix in the reference's summation order (mass.h:160-170,
+     matrix_creator.h:45-50): q outer, cell_matrix(i, j) += (phi_i phi_j) JxW
+     for mass, (grad phi_i . grad phi_j) JxW for Laplace. On the uniform mesh
+     the matrix depends only on the category tuple, so it is computed once per
+     tuple present (bit-identical to recomputing it per cell; the tuples are
+     independent, so they run in parallel), then scattered in cell order. */
+  unsigned *keys = (unsigned *)malloc(sizeof(unsigned) * ncat * ncat * ncat);
+  unsigned (*kcat)[3] = malloc(sizeof(unsigned[3]) * ncat * ncat * ncat);
+  int n_keys = 0;
+  double h[3];
   for (unsigned c = 0; c < nc; ++c) {
     unsigned cidx[3], cat[3];
-    double h[3];
     cell_setup(dim, p, nsub, c, lo, hi, cidx, cat, h);
-    /* the tensor-product QGauss(p+1) element matrix, sum-factorised: 1D mass
-       M_d[i][j] = h_d sum_q w_q v_i v_j and stiffness K_d[i][j] = 1 / h_d
-       sum_q w_q v_i' v_j' per direction; mass = M_z x M_y x M_x, Laplace =
-       sum_e (K_e in direction e, M elsewhere) -- the same quadrature sums as
-       the cell loop, in a different order */
-    double M1[3][MAXN][MAXN], K1[3][MAXN][MAXN];
-    for (int d = 0; d < dim; ++d)
-      for (int i = 0; i < n1; ++i)
-        for (int j = 0; j < n1; ++j) {
-          double m = 0.0, k = 0.0;
-          for (int q = 0; q < n1; ++q) {
-            m += T.wq[q] * T.v1[cat[d]][i][q] * T.v1[cat[d]][j][q];
-            k += T.wq[q] * T.g1[cat[d]][i][q] * T.g1[cat[d]][j][q];
-          }
-          M1[d][i][j] = m * h[d];
-          K1[d][i][j] = k / h[d];
-        }
+    const unsigned key = cat[0] + ncat * (cat[1] + ncat * cat[2]);
+    if (!cache[key]) {
+      cache[key] = (double *)calloc((size_t)nd * nd, sizeof(double));
+      keys[n_keys] = key;
+      memcpy(kcat[n_keys], cat, sizeof(cat));
+      ++n_keys;
+    }
+  }
+  double jxw_vol = 1.0;
+  for (int d = 0; d < dim; ++d)
+    jxw_vol *= h[d];
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int t = 0; t < n_keys; ++t) {
+    const unsigned *cat = kcat[t];
+    double *m = cache[keys[t]];
+    double *svT = (double *)malloc(sizeof(double) * nd * nd);
+    double *sg = kind == 0 ? NULL : (double *)malloc(sizeof(double) * nd * nd * 3);
     for (int i = 0; i < nd; ++i)
-      for (int j = 0; j < nd; ++j) {
-        int ii[3] = {0, 0, 0}, jj[3] = {0, 0, 0}, ri = i, rj = j;
-        for (int d = 0; d < dim; ++d) {
-          ii[d] = ri % n1;
-          ri /= n1;
-          jj[d] = rj % n1;
-          rj /= n1;
-        }
-        double s;
+      for (int q = 0; q < nd; ++q)
+        shape_at(&T, cat, i, q, h, &svT[q * nd + i], kind == 0 ? NULL : &sg[3 * (i * nd + q)]);
+    for (int q = 0; q < nd; ++q) {
+      int rq = q;
+      double wq = jxw_vol;
+      for (int d = 0; d < dim; ++d) {
+        wq *= T.wq[rq % n1];
+        rq /= n1;
+      }
+      const double *sq = &svT[q * nd];
+      for (int i = 0; i < nd; ++i) {
+        double *mi = &m[(size_t)i * nd];
         if (kind == 0) {
-          s = 1.0;
-          for (int d = 0; d < dim; ++d) s *= M1[d][ii[d]][jj[d]];
+          const double a = sq[i];
+          for (int j = 0; j < nd; ++j)
+            mi[j] += a * sq[j] * wq;
         } else {
-          s = 0.0;
-          for (int e = 0; e < dim; ++e) {
-            double t = 1.0;
-            for (int d = 0; d < dim; ++d) t *= (d == e ? K1[d] : M1[d])[ii[d]][jj[d]];
-            s += t;
+          const double *gi = &sg[3 * (i * nd + q)];
+          for (int j = 0; j < nd; ++j) {
+            const double *gj = &sg[3 * (j * nd + q)];
+            double s = 0.0;
+            for (int e = 0; e < dim; ++e)
+              s += gi[e] * gj[e];
+            mi[j] += s * wq;
           }
         }
-        cm[i * nd + j] = s;
       }
+    }
+    free(svT);
+    free(sg);
+  }
+  free(keys);
+  free(kcat);
+  for (unsigned c = 0; c < nc; ++c) {
+    unsigned cidx[3], cat[3];
+    cell_setup(dim, p, nsub, c, lo, hi, cidx, cat, h);
+    const unsigned key = cat[0] + ncat * (cat[1] + ncat * cat[2]);
+    const double *cm = cache[key];
     gdmo_cell_dof_indices(dim, p, nsub, c, dofs);
     for (int i = 0; i < nd; ++i) {
       /* row r's columns are its |i_d - j_d| <= p box, sorted z, y, x: the
@@ -855,8 +881,10 @@ int64_t gdmo_matrix_csr(int dim, int p, const unsigned *nsub, const double *lo, 
       }
     }
   }
+  for (unsigned k = 0; k < ncat * ncat * ncat; ++k)
+    free(cache[k]);
+  free(cache);
   free(dofs);
-  free(cm);
   return nnz;
 }
 
@@ -877,8 +905,11 @@ void gdmo_csr_vmult(int64_t n, const int64_t *rowptr, const int64_t *cols, const
 /* precond: 0 identity, 1 Jacobi (PreconditionJacobi, omega = 1).             */
 /* Returns the number of iterations (last_step), or -1 on no convergence.     */
 /* ------------------------------------------------------------------------- */
-int gdmo_cg(int64_t n, const int64_t *rowptr, const int64_t *cols, const double *vals,
-            const double *b, double *x, int precond, int max_it, double abs_tol, double rel_tol)
+/* hist (nullable, max_it + 1 entries): the residual norm before iteration 1
+   and after every iteration; *tol_out (nullable): the stopping threshold. */
+int gdmo_cg_history(int64_t n, const int64_t *rowptr, const int64_t *cols, const double *vals,
+                    const double *b, double *x, int precond, int max_it, double abs_tol, double rel_tol,
+                    double *hist, double *tol_out)
 {
   double *r = (double *)malloc(sizeof(double) * n);
   double *pv = (double *)malloc(sizeof(double) * n);
@@ -899,6 +930,10 @@ int gdmo_cg(int64_t n, const int64_t *rowptr, const int64_t *cols, const double 
   }
   res = sqrt(res);
   const double tol = fmax(abs_tol, rel_tol * res);
+  if (hist)
+    hist[0] = res;
+  if (tol_out)
+    *tol_out = tol;
   int it = 0, ret = -1;
   if (res <= tol) {
     ret = 0;
@@ -932,6 +967,8 @@ int gdmo_cg(int64_t n, const int64_t *rowptr, const int64_t *cols, const double 
       res += r[i] * r[i];
     }
     res = sqrt(res);
+    if (hist)
+      hist[it] = res;
     if (res <= tol) {
       ret = it;
       break;
@@ -943,6 +980,12 @@ done:
   free(v);
   free(dinv);
   return ret;
+}
+
+int gdmo_cg(int64_t n, const int64_t *rowptr, const int64_t *cols, const double *vals,
+            const double *b, double *x, int precond, int max_it, double abs_tol, double rel_tol)
+{
+  return gdmo_cg_history(n, rowptr, cols, vals, b, x, precond, max_it, abs_tol, rel_tol, NULL, NULL);
 }
 
 /* ------------------------------------------------------------------------- */

@@ -56,6 +56,8 @@ def lib():
         L.gdmo_csr_vmult.argtypes = [i64, P, P, P, P, P]
         L.gdmo_cg.restype = i
         L.gdmo_cg.argtypes = [i64, P, P, P, P, P, i, i, d, d]
+        L.gdmo_cg_history.restype = i
+        L.gdmo_cg_history.argtypes = [i64, P, P, P, P, P, i, i, d, d, P, P]
         L.gdmo_l2_error.restype = d
         L.gdmo_l2_error.argtypes = [i, i, P, P, P, P, P]
         L.gdmo_error_norms.argtypes = [i, i, P, P, P, P, P, P, P]
@@ -257,6 +259,21 @@ def cg(rowptr, cols, vals, b, x=None, precond=0, max_it=1000, abs_tol=1e-20, rel
     b = np.ascontiguousarray(b, dtype=np.float64)
     its = lib().gdmo_cg(n, _p(rowptr), _p(cols), _p(vals), _p(b), _p(x), precond, max_it, abs_tol, rel_tol)
     return x, its
+
+
+def cg_history(rowptr, cols, vals, b, precond=0, max_it=1000, abs_tol=1e-20, rel_tol=1e-14):
+    """cg() from a zero start that also returns the residual norm history
+    (hist[0] before iteration 1, hist[k] after iteration k) and the stopping
+    threshold max(abs_tol, rel_tol |r_0|) of deal.II's ReductionControl."""
+    n = len(rowptr) - 1
+    x = np.zeros(n)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    hist = np.full(max_it + 1, np.nan)
+    tol = np.zeros(1)
+    its = lib().gdmo_cg_history(n, _p(rowptr), _p(cols), _p(vals), _p(b), _p(x), precond, max_it, abs_tol,
+                                rel_tol, _p(hist), _p(tol))
+    last = its if its >= 0 else max_it
+    return x, its, hist[:last + 1], float(tol[0])
 
 
 def csr_vmult(rowptr, cols, vals, x):

@@ -6,9 +6,12 @@
     pinned to mass_0x / poisson_01 goldens) and on ragged random matrices
     (empty rows, long rows, rectangular, nnz = 0).  fp64 summation order is the
     only difference, hence the tolerance.
-  * CG: deal.II SolverCG + ReductionControl semantics (oracle gdmo_cg): same
-    iteration count (+-1 for rounding at the stopping threshold) and the
-    solutions agree to the solver tolerance.
+  * CG: deal.II SolverCG + ReductionControl semantics (oracle gdmo_cg): the
+    device's stopping iteration is where the oracle's residual history
+    crosses the threshold (within 1 % of it at rel 1e-6, a factor 2 at rel
+    1e-14 where rounding of the residual recurrence is of the order of tol;
+    _cg_stop_ok), and the solutions
+    agree to the solver tolerance when the counts are equal.
   * triplet files (wave-ev.cc:93-127): bit-exact round trip, deal.II entry order.
   * config 5 size (2D p=3, 4096^2 vertices, full structural stencil): the
     device SpMV equals the same Kronecker operator applied as a 7x7 fp64
@@ -130,6 +133,17 @@ def _sum_csr(a, b):
     return a[0], a[1], a[2] + b[2]
 
 
+def _cg_stop_ok(k, hist, tol, slack):
+    """The device's stopping iteration k is consistent with the oracle's
+    residual history when the oracle's residual at k is below the threshold
+    (within the factor 1 + slack) and every earlier residual is above it
+    (within the same factor): identity-CG residuals are not monotone, so an
+    exact +-1 window flips on ulp-level changes of the matrix."""
+    if k >= len(hist):
+        return False
+    return hist[k] <= tol * (1 + slack) and bool(np.all(hist[:k] > tol / (1 + slack)))
+
+
 @pytest.mark.parametrize("dim,p,n", [(1, 3, 64), (2, 3, 16), (2, 5, 12), (3, 3, 7)])
 @pytest.mark.parametrize("precond", ["identity", "jacobi"])
 def test_cg_vs_oracle(dim, p, n, precond):
@@ -142,8 +156,21 @@ def test_cg_vs_oracle(dim, p, n, precond):
     lap_mass = _sum_csr(m.matrix_csr(kind=1), mass)
     pc = 1 if precond == "jacobi" else 0
     for (rp, cols, vals), abs_tol, rel_tol in ((mass, 1e-20, 1e-14), (lap_mass, 1e-10, 1e-6)):
-        x_ref, its_ref = O.cg(rp, cols, vals, b, precond=pc, max_it=5000, abs_tol=abs_tol, rel_tol=rel_tol)
+        x_ref, its_ref, _, tol = O.cg_history(rp, cols, vals, b, precond=pc, max_it=5000, abs_tol=abs_tol,
+                                              rel_tol=rel_tol)
         assert its_ref > 0
+        # Band around tol inside which rounding decides the crossing.  At rel
+        # 1e-6 the recurrence residuals of two summation orders agree to far
+        # better than 1 %.  At rel 1e-14 the recurrence's rounding (about
+        # eps kappa |b|) is itself of the order of tol: device and oracle
+        # residuals there differ by up to ~2x (3D p=3 Jacobi mass: the
+        # device stops at 64, where the oracle's residual is 1.42 tol), so
+        # the band is a factor 2, about one iteration of the decay.
+        slack = 1e-2 if rel_tol >= 1e-10 else 1.0
+        # the same iterates run past the threshold (a lower one) for the
+        # residuals after its_ref
+        _, _, hist, _ = O.cg_history(rp, cols, vals, b, precond=pc, max_it=5000, abs_tol=abs_tol / (1 + slack),
+                                     rel_tol=rel_tol / (1 + slack))
         A = sp.SparseMatrix(rp, cols.astype(np.uint32), vals)
         # repeated solves: the round-1 defect (a scalar slot read and written
         # in one kernel) showed up in some runs only
@@ -151,7 +178,7 @@ def test_cg_vs_oracle(dim, p, n, precond):
             x = torch.zeros(m.n_dofs, dtype=torch.float64, device="cuda")
             its, res = sp.solve_cg(A, x, dev(b), preconditioner=precond, max_it=5000, abs_tol=abs_tol,
                                    rel_tol=rel_tol)
-            assert abs(its - its_ref) <= 1, (its, its_ref)
+            assert _cg_stop_ok(its, hist, tol, slack), (its, its_ref, hist[max(its - 2, 0):its + 2] / tol)
             if its == its_ref:
                 assert rel(host(x), x_ref) < (1e-10 if rel_tol < 1e-12 else 1e-7)
             r = b - O.csr_vmult(rp, cols, vals, host(x))

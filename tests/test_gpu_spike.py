@@ -85,3 +85,32 @@ def test_slab_mass_solve_refuses_slabs_thinner_than_2p():
     x = op.new_vector(False)
     with pytest.raises(gdm_amd.GdmError, match="too thin"):
         op.mass_solve_slab(x, x)
+
+
+def test_interface_refuses_skipped_or_out_of_order_rounds():
+    """The C4 partition needs one refinement round: an interface call without
+    it, a round before the slab solve, a round out of order and a second
+    interface call after one solve are refused (GDM_ERR_STATE) instead of a
+    silently wrong inverse from stale saved edge planes."""
+    import gdm_amd
+
+    n, R = (8, 9, 255), 8
+    assert gdm_amd._capi.mass_spike_rounds(3, 7, n, R) == 1
+    op = gdm_amd.GdmOperator(3, 7, n, 0.0, 1.0, "mass", n_ranks=R, rank=3)
+    x = op.new_vector(True)
+    r = torch.ones(op.n_owned, dtype=torch.float64, device="cuda")
+    with pytest.raises(gdm_amd.GdmError, match="gdm_mass_solve_slab first"):
+        op.mass_solve_interface_round(x, 0)
+    op.mass_solve_slab(r, op.owned_view(x))
+    with pytest.raises(gdm_amd.GdmError, match="0 of 1 refinement rounds"):
+        op.mass_solve_interface(x)
+    op.mass_solve_interface_round(x, 0)
+    with pytest.raises(gdm_amd.GdmError, match="in order"):
+        op.mass_solve_interface_round(x, 0)
+    op.mass_solve_interface(x)
+    with pytest.raises(gdm_amd.GdmError, match="gdm_mass_solve_slab first"):
+        op.mass_solve_interface(x)
+    # SlabMassSolve without an explicit count asks the C ABI for it
+    from gdm_amd.distributed import SlabMassSolve
+
+    assert SlabMassSolve(op, None).rounds == 1
