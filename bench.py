@@ -46,7 +46,8 @@ def parse():
     ap.add_argument("--kind", default="advection", choices=["advection", "wave", "mass"])
     ap.add_argument("--strong", action="store_true", help="(default for N > 1) fixed 512^3 global grid")
     ap.add_argument("--weak", action="store_true", help="one 512-plane slab per GPU instead of a fixed global grid")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0: min(16, nproc))")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: nproc, bounded by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cells", type=int, default=24, help="cells per direction of the CPU-baseline sample")
     ap.add_argument("--pmc", default=os.environ.get("GDM_BENCH_PMC", "1"), help="collect HBM PMC traffic (1/0)")
@@ -78,7 +79,7 @@ def _timed(fn, budget):
     return (time.perf_counter() - t0) / reps, reps
 
 
-def cpu_baseline(p, n_cells, threads):
+def cpu_baseline(p, n_cells, threads, threads_source="--cpu-threads"):
     """Reference algorithms from the CPU restatement in oracle/ (test
     infrastructure, the checker -- never the measured product), on bounded
     samples of the benchmark's workloads:
@@ -105,6 +106,8 @@ def cpu_baseline(p, n_cells, threads):
 
     a = (1.0, 0.15, -0.05)
     O.Mesh(3, p, p + 1).advection_rhs(a, np.zeros((p + 2) ** 3), None)  # load the library
+    # every thread gets at least one z-layer of cells (a larger sample on a larger host)
+    n_cells = max(n_cells, threads)
     m = O.Mesh(3, p, n_cells, 0.0, 1.0)
     u = np.random.default_rng(20251010).uniform(-1, 1, m.n_dofs)
     bounds = [(n_cells * t // threads, n_cells * (t + 1) // threads) for t in range(threads)]
@@ -118,7 +121,7 @@ def cpu_baseline(p, n_cells, threads):
         m.advection_rhs(a, u, bcs[t], cb=cb, ce=ce, rhs=outs[t])
 
     # C4 sample: wave p=7 cell loop, z-slabs over the same threads
-    nw = 12
+    nw = max(12, threads)
     mw = O.Mesh(3, 7, nw, -1.21, 1.21)
     uw = np.random.default_rng(5).uniform(-1, 1, mw.n_dofs)
     wb = [(nw * t // threads, nw * (t + 1) // threads) for t in range(threads)]
@@ -165,6 +168,7 @@ def cpu_baseline(p, n_cells, threads):
         "value": m.n_dofs / dt_n,
         "unit": "DoF-updates/s",
         "cores": threads,
+        "cores_source": threads_source,
         "cores_visible": os.cpu_count(),
         "cores_nproc": _nproc(),
         "kind": "port",
@@ -182,6 +186,10 @@ def cpu_baseline(p, n_cells, threads):
                               "%d application(s)" % (nw, threads, reps_w)},
         "c5_cg": {"value": (n5 * n5) / dt5, "unit": "row-updates/s (one CG iteration = SpMV + 2 dots + 3 axpys)",
                   "ms_per_iteration": dt5 * 1e3, "cores": 1,
+                  # C5 is 4096^2: a CG iteration is linear in the rows (fixed (2p+1)^2 entries per row), so the
+                  # 1024^2 sample's time per row is extrapolated x16 (the 4096^2 CSR would need ~13 GB of host
+                  # memory and minutes of assembly inside the bench)
+                  "ms_per_iteration_c5_extrapolated": dt5 * 1e3 * (4096 * 4096) / (n5 * n5),
                   "sample": "2D p=3 %d^2 DoFs, CSR %d nnz (full (2p+1)^2 GDM sparsity), SolverCG + "
                             "PreconditionIdentity, %d iterations, 1 thread" % (n5, len(v5), its5)},
     }
@@ -243,6 +251,38 @@ def _nproc():
         return len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         return os.cpu_count() or 1
+
+
+def _cgroup_cpus():
+    """CPUs the cgroup's CFS quota allots this process (cgroup v2 cpu.max or
+    v1 cpu.cfs_quota_us / cpu.cfs_period_us), with the file it came from;
+    (None, None) when unlimited or unreadable."""
+    import math
+
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(per))), "/sys/fs/cgroup/cpu.max"
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, math.ceil(q / per)), "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"
+    except (OSError, ValueError):
+        pass
+    return None, None
+
+
+def cpu_threads():
+    """Threads of the CPU baseline: the affinity mask (nproc), bounded by the
+    cgroup's CPU quota when there is one; returns (threads, source)."""
+    n = _nproc()
+    cg, src = _cgroup_cpus()
+    if cg is not None and cg < n:
+        return cg, "cgroup quota (%s)" % src
+    return n, "sched_getaffinity (nproc)"
 
 
 def _cpu_model():
@@ -412,9 +452,9 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not args.metric_only:
         try:
-            # every CPU this process may run on (nproc = the affinity mask), capped at the 16 host CPUs the
-            # GPU box allots per GPU (os.cpu_count() shows the whole machine there)
-            cpu = cpu_baseline(p, args.cpu_cells, args.cpu_threads or min(16, _nproc()))
+            # every CPU this process may run on: the affinity mask (nproc), bounded by the cgroup's CPU quota
+            th, src = (args.cpu_threads, "--cpu-threads") if args.cpu_threads else cpu_threads()
+            cpu = cpu_baseline(p, args.cpu_cells, th, src)
         except Exception as e:  # the baseline never blocks the GPU line
             cpu = {"value": None, "error": str(e)}
     out = {

@@ -734,6 +734,10 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
 #ifdef GDM_DIAG
   if (const char *env = std::getenv("GDM_DBG")) a.dbg = std::atoi(env);
 #endif
+#ifdef GDM_STAMP
+  a.stamps = nullptr;
+  if (const char *env = std::getenv("GDM_STAMP_PTR")) a.stamps = (unsigned long long *)std::strtoull(env, nullptr, 0);
+#endif
   if (L.n_owned == 0) return hipSuccess;
   const int bk = as_mass ? 0 : (op->kind == GDM_OP_WAVE ? 2 : 1);
   if (!v8) {
@@ -2228,6 +2232,14 @@ int64_t gdmh_band_cholesky(int64_t n, const int64_t *rp, const uint32_t *ci, con
                            const int64_t *rp2, const uint32_t *ci2, const double *v2, std::vector<double> &lband);
 }
 
+// message for a failed gdmh_band_cholesky (-1: not positive definite, -2: too large)
+static std::string band_error(int64_t code, const char *what) {
+  return std::string("cut wave: ") + what +
+         (code == -2 ? ": banded factor larger than 2^28 entries (mesh too large for the dense-band solve)"
+                     : " not positive definite");
+}
+
+
 namespace {
 struct DevCsr {
   int64_t rows = 0;
@@ -2344,7 +2356,7 @@ int gdm_cut_wave_create(int dim, int fe_degree, int n_subdivisions, double left,
       gdmh_cut_wave_csr(c->host, 4, &rp, &ci, &v);
       std::vector<double> lb;
       c->bw_m = gdmh_band_cholesky(c->n_dofs, rp, ci, v, 0.0, nullptr, nullptr, nullptr, lb);
-      if (c->bw_m < 0) throw std::runtime_error("cut wave: mass matrix not positive definite");
+      if (c->bw_m < 0) throw std::runtime_error(band_error(c->bw_m, "mass matrix"));
       c->lband_m = dev_upload(lb);
     }
   } catch (...) {
@@ -2452,7 +2464,7 @@ int gdm_cut_wave_system_solve(gdm_cut_wave *c, double dt, const double *rhs, dou
     gdmh_cut_wave_csr(c->host, 5, &rp2, &ci2, &v2);
     std::vector<double> lb;
     const int64_t bw = gdmh_band_cholesky(c->n_dofs, rp, ci, v, dt, rp2, ci2, v2, lb);
-    if (bw < 0) throw std::runtime_error("cut wave: M + dt K not positive definite");
+    if (bw < 0) throw std::runtime_error(band_error(bw, "M + dt K"));
     // the previous factor may still be read by queued solves
     hip_check(hipStreamSynchronize(c->op->stream), "hipStreamSynchronize");
     if (c->lband_a) (void)hipFree(c->lband_a);
@@ -2478,7 +2490,7 @@ int gdm_cut_wave_stiffness_solve(gdm_cut_wave *c, const double *rhs, double *x) 
     gdmh_cut_wave_csr(c->host, 5, &rp, &ci, &v);
     std::vector<double> lb;
     const int64_t bw = gdmh_band_cholesky(c->n_dofs, rp, ci, v, 0.0, nullptr, nullptr, nullptr, lb);
-    if (bw < 0) throw std::runtime_error("cut wave: stiffness matrix not positive definite");
+    if (bw < 0) throw std::runtime_error(band_error(bw, "stiffness matrix"));
     c->lband_k = dev_upload(lb);
     c->bw_k = bw;
   }

@@ -509,7 +509,9 @@ void assemble2d(gdm_cut_wave_system &S, const double *ls_values) {
 extern "C" {
 
 // banded Cholesky of a CSR SPD matrix (half-bandwidth taken from the pattern):
-// lband [n][bw + 1], L(i, i - bw + k); returns bw, or -1 if not positive definite
+// lband [n][bw + 1], L(i, i - bw + k); returns bw, -1 if not positive definite,
+// -2 if n (bw + 1) exceeds kBandMaxEntries (the mesh is too large for the dense band)
+constexpr int64_t kBandMaxEntries = int64_t(1) << 28;
 int64_t gdmh_band_cholesky(int64_t n, const int64_t *rp, const uint32_t *ci, const double *v, double alpha,
                            const int64_t *rp2, const uint32_t *ci2, const double *v2, std::vector<double> &lband);
 
@@ -603,6 +605,10 @@ int64_t gdmh_band_cholesky(int64_t n, const int64_t *rp, const uint32_t *ci, con
       for (int64_t q = rp2[r]; q < rp2[r + 1]; ++q) bw = std::max<int64_t>(bw, r - (int64_t)ci2[q]);
   }
   const int64_t W = bw + 1;
+  // the band is dense inside (O(n bw) memory, O(n bw^2) work, bw ~ p (n_sub + 1)
+  // in 2D): refuse factors beyond kBandMaxEntries doubles (2 GiB) instead of an
+  // out-of-memory death or a multi-hour factorisation
+  if (n * W > kBandMaxEntries) return -2;
   std::vector<double> A((size_t)n * W, 0.0);
   for (int64_t r = 0; r < n; ++r) {
     for (int64_t q = rp[r]; q < rp[r + 1]; ++q)

@@ -68,6 +68,30 @@ namespace gdmk {
 #define GDM_DBG(a, bit) false
 #endif
 #define GDM_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+// stamp builds (-DGDM_STAMP, tools/stamp_stencil.py): s_memtime of every wave
+// at the phase boundaries of planes [STAMP_I0, STAMP_I0 + STAMP_NI) of every
+// workgroup, stored by lane 0 (vector store) to a.stamps[((sid * NI + i) *
+// 16 + wave) * 8 + slot].  Timing shares only: the stamps' waits change the
+// kernel.
+#ifdef GDM_STAMP
+#define STAMP_I0 40
+#define STAMP_NI 24
+#define GDM_STAMPT(t_, i_, slot_)                                                                    \
+  do {                                                                                               \
+    if (a.stamps && (i_) >= STAMP_I0 && (i_) < STAMP_I0 + STAMP_NI) {                                \
+      unsigned long long ts_;                                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");                      \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+      if ((t_).lane == 0)                                                                            \
+        a.stamps[(((int64_t)(t_).sid * STAMP_NI + ((i_)-STAMP_I0)) * 16 + (t_).wv) * 8 + (slot_)] = ts_; \
+    }                                                                                                \
+  } while (0)
+#else
+#define GDM_STAMPT(t_, i_, slot_) \
+  do {                            \
+  } while (0)
+#endif
 
 // Coefficient tables are read-only for the whole launch and indexed by
 // wave-uniform positions: read them through the constant address space so
@@ -156,6 +180,8 @@ typedef __attribute__((address_space(3))) const dpair lcdouble2;
 
 struct Tile7 {
   ldouble *u0, *ab0, *zt, *yc, *corr, *yw;
+  int sid;  // stamp builds: logical workgroup id
+  int cw;   // v8 / v9: this wave's output row block (rows cw R .. cw R + R - 1 of the tile)
   bool yedge;  // v8: the tile has rows next to a y wall
   int lane, wv, x0, y0, zc0, zc1, zs, ze, zend;
   // x wall columns inside this tile: nl from the left wall, nr from column rs on
@@ -456,6 +482,7 @@ __device__ __forceinline__ void cplane7(const StencilArgs &a, const Tile7 &t, bo
   // The ring values only feed the conditional retire stores; without this
   // opaque use LLVM sinks each slot's whole FMA chain into its store branch
   // and keeps every plane's D/E and coefficients alive until then.
+  GDM_STAMPT(t, zz - t.zs, 3);
 #pragma unroll
   for (int s = 0; s < W; ++s)
 #pragma unroll
@@ -477,6 +504,7 @@ __device__ __forceinline__ void cplane7(const StencilArgs &a, const Tile7 &t, bo
   }
 #pragma unroll
   for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
+  GDM_STAMPT(t, zz - t.zs, 4);
 }
 
 template <int JP, int P, int R, int NC, int NP, int BK>
@@ -657,6 +685,17 @@ template <int P, int BK>
 __device__ __forceinline__ constexpr double zband(int k) {
   using IR = InteriorRows<P>;
   return BK == 0 ? IR::m[2 * P - k] : (BK == 1 ? IR::c[2 * P - k] : IR::l[2 * P - k]);
+}
+
+// run-time interior band coefficient k of kind BK from its first half: the
+// bands are symmetric (mass, wave) or antisymmetric (advection, c[p] = 0), and
+// the host tables (cy8, zd8, m_zd8: a scale times the band) inherit that
+// exactly, so only p + 1 SGPR pairs stay live (the negation is an operand
+// modifier of the FMA)
+template <int P, int BK>
+__device__ __forceinline__ double hcoef(const double *c, int k) {
+  if (k <= P) return c[k];
+  return BK == 1 ? -c[2 * P - k] : c[2 * P - k];
 }
 
 // wait until at most K planes of DMA of this producer wave are in flight
@@ -878,6 +917,7 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
     if (t.ncw > 0) xwall8_pre<P, R, NC, NP, BK>(a, t, xpre);
     for (int i = 0; i < n; ++i) {
       const int slot = i & 1;
+      GDM_STAMPT(t, i, 0);
       if (GDM_DBG(a, 8))
         ;
       else if (i + 1 < n)
@@ -886,6 +926,7 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
         GDM_WAIT_VMCNT(0);
       Tile7 tt = t;
       tt.ab0 = t.ab0 + slot * G::ABSZ;
+      GDM_STAMPT(t, i, 1);
 #pragma unroll
       for (int ps = 0; ps < G::NPASS; ++ps) {
         const int g = t.wv + ps * NP;
@@ -903,8 +944,11 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
       // reads of them have returned (before B_i: the barrier wait then
       // overlaps the fetch)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      GDM_STAMPT(t, i, 2);
       if (i + 2 < n && !GDM_DBG(a, 8)) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre);
-      GDM_LDS_BARRIER();  // B_i: AB(i) complete
+      GDM_STAMPT(t, i, 3);
+      if (!GDM_DBG(a, 16)) GDM_LDS_BARRIER();  // B_i: AB(i) complete
+      GDM_STAMPT(t, i, 4);
       if (t.yedge) {
         ywall8<P, R, NC, NP, BK>(a, tt);
         GDM_LDS_BARRIER();  // M_i
@@ -922,7 +966,7 @@ __device__ __forceinline__ void ysweep8(const StencilArgs &a, const Tile7 &t, do
   using G = Geom8<P, R, NC, NP, BK>;
   using IR = InteriorRows<P>;
   constexpr int W = G::W, TX = G::TX, NR = R + 2 * P;
-  const int row0 = (t.wv - NP) * R;
+  const int row0 = t.cw * R;
 #pragma unroll
   for (int j = 0; j < R; ++j) D[j] = E[j] = 0.0;
   if constexpr (BK != 0) {
@@ -942,7 +986,7 @@ __device__ __forceinline__ void ysweep8(const StencilArgs &a, const Tile7 &t, do
           if (BK == 1 && k == P)  // cy[p] = h_x a_y chat[p] = 0
             E[j] = fma(IR::m[k], v[s].y, E[j]);
           else
-            E[j] = fma(IR::m[k], v[s].y, fma(a.cy[k], v[s].x, E[j]));
+            E[j] = fma(IR::m[k], v[s].y, fma(hcoef<P, BK>(a.cy, k), v[s].x, E[j]));
         }
       }
     }
@@ -972,7 +1016,9 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
   constexpr int W = G::W;
   if (zz < t.ze) {
     double D[R], E[R];
+    GDM_STAMPT(t, zz - t.zs, 0);
     GDM_LDS_BARRIER();  // L_i (DB: B_i)
+    GDM_STAMPT(t, zz - t.zs, 1);
     Tile7 tt = t;
     tt.ab0 = t.ab0 + ((zz - t.zs) & 1) * G::ABSZ;
     if (GDM_DBG(a, 1)) {
@@ -981,6 +1027,7 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
     } else {
       ysweep8<P, R, NC, NP, BK, PF>(a, tt, D, E);
     }
+    GDM_STAMPT(t, zz - t.zs, 2);
     if constexpr (YW) {
       GDM_LDS_BARRIER();  // M_i
       const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
@@ -1009,11 +1056,11 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
 #pragma unroll
           for (int j = 0; j < R; ++j) {
             if constexpr (BK == 0)
-              acc[slot][j] = fma(a.zd[k], D[j], acc[slot][j]);
+              acc[slot][j] = fma(hcoef<P, BK>(a.zd, k), D[j], acc[slot][j]);
             else if (zband<P, BK>(k) == 0.0)
               acc[slot][j] = fma(IR::m[k], E[j], acc[slot][j]);
             else
-              acc[slot][j] = fma(IR::m[k], E[j], fma(a.zd[k], D[j], acc[slot][j]));
+              acc[slot][j] = fma(IR::m[k], E[j], fma(hcoef<P, BK>(a.zd, k), D[j], acc[slot][j]));
           }
         }
       } else {
@@ -1057,6 +1104,7 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
       }
     }
   }
+  GDM_STAMPT(t, zz - t.zs, 3);
 #pragma unroll
   for (int s = 0; s < W; ++s)
 #pragma unroll
@@ -1078,6 +1126,7 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
   }
 #pragma unroll
   for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
+  GDM_STAMPT(t, zz - t.zs, 4);
 }
 
 template <int JP, int P, int R, int NC, int NP, int BK, int PF, bool WALL, bool YW>
@@ -1112,7 +1161,7 @@ __device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7
 template <int P, int R, int NC, int NP, int BK, int PF, bool ZI>
 __device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) {
   using G = Geom8<P, R, NC, NP, BK>;
-  const int ybase = t.y0 + (t.wv - NP) * R;
+  const int ybase = t.y0 + t.cw * R;
   const bool full = (t.x0 + G::TX <= a.Nx) && (ybase + R <= a.out_y1);
   // edge tiles (rows next to a y wall) wait for the producers' y-wall
   // corrections every plane: their own copy of the loop keeps that out of the
@@ -1139,6 +1188,7 @@ __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, N
   t.yw = lds + G::OFF_YW;
   t.lane = threadIdx.x & 63;
   t.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  t.cw = t.wv - NP;
   // XCD-aware tile order: the hardware deals workgroup b to XCD b % 8; XCD k
   // gets the contiguous logical range [k q, (k + 1) q) of tiles (x fastest),
   // so the tiles sharing x- and y-halo lines run on one XCD at the same time
@@ -1153,6 +1203,7 @@ __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, N
     by = (int)((L / gx) % gy);
     bz = (int)(L / (gx * gy));
   }
+  t.sid = bx + gridDim.x * (by + gridDim.y * bz);
   t.x0 = bx * G::TX;
   t.y0 = a.out_y0 + by * G::TY;
 #ifdef GDM_EXP_NOY
@@ -1200,6 +1251,357 @@ __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, N
   else
     consumer8<P, R, NC, NP, BK, PF, ZI>(a, t);
 #endif
+}
+
+// ===========================================================================
+// Fused Kronecker stencil, v9: every wave plays both roles.
+//
+// s_memtime stamps of v8 (tools/stamp_stencil.py, profiles/r4b) showed its
+// producer waves parked at the plane barrier for ~60 % of every plane while
+// the consumers' y/z FMA chains set the period.  Here all NW = 16 waves own R
+// = 2 output rows (the z ring is 2p+1 planes x 2 rows, so it fits beside the
+// x-sweep's registers) and the first NG waves also run the x-sweep of one
+// 4-row group: every SIMD keeps four waves with work, and the x-sweep's
+// independent FMAs fill the latency of the y/z chains.  One barrier per plane:
+//   B_i | Y(i) (+ own y-wall rows) | Z(i) | retire | [w < NG] X(i+1) -> AB (i+1)&1, DMA(i+3)
+// X(i+1) overwrites the AB buffer that every wave read in Y(i-1), before B_i.
+// Output rows are written with buffer stores (out-of-range lanes dropped by
+// the resource's bound), so every retire issues exactly R stores and the
+// counted vmcnt before X(i+1) stays exact.
+// ===========================================================================
+#ifndef GDM_V9_XF
+#define GDM_V9_XF 1
+#endif
+template <int P, int R, int NW, int BK>
+using Geom9 = Geom8<P, R, NW, NW, BK>;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// wait until the DMA of the plane the next x-sweep reads has landed: the
+// VMEM instructions issued after it are the `stores` buffer stores since then
+// plus, if next_dma, the DMA of the following plane (nd instructions)
+template <int N, int R>
+__device__ __forceinline__ void wait_vm9(int stores) {
+  if (stores <= 0) GDM_WAIT_VMCNT(N);
+  else if (stores <= R) GDM_WAIT_VMCNT(N + R);
+  else if (stores <= 2 * R) GDM_WAIT_VMCNT(N + 2 * R);
+  else if (stores <= 3 * R) GDM_WAIT_VMCNT(N + 3 * R);
+  else GDM_WAIT_VMCNT(N + 4 * R);
+}
+
+template <int I, int P, int R, int NW, int BK, int CH>
+__device__ __forceinline__ void wait_dma9(int wv, bool next_dma, int stores) {
+  if constexpr (I < NW) {
+    if (wv == I) {
+      if (next_dma)
+        wait_vm9<Dma7<P, R, NW, NW, BK, CH>::nd(I), R>(stores);
+      else
+        wait_vm9<0, R>(stores);
+      return;
+    }
+    wait_dma9<I + 1, P, R, NW, BK, CH>(wv, next_dma, stores);
+  }
+}
+
+// x-sweep of this wave's row group g = wv of the plane in u slot `us` into
+// the AB buffer `ab` (+ x-wall corrections on wall tiles)
+template <int P, int R, int NW, int BK>
+__device__ __forceinline__ void xstep9(const StencilArgs &a, const Tile7 &t, lcdouble *us, ldouble *ab,
+                                       const XWallPre<P, BK> &xpre) {
+  Tile7 tt = t;
+  tt.ab0 = ab;
+  dpair V[4];
+  xsweep8<P, R, NW, NW, BK>(a, tt, us, t.wv, V);
+  write_ab8<P, R, NW, NW, BK>(tt, t.wv, V);
+  if (t.ncw > 0) {
+    XWall<P, BK> xw;
+    xwall8_calc<P, R, NW, NW, BK>(tt, us, t.wv, xpre, xw);
+    xwall8_add<P, BK>(tt, xw);
+  }
+}
+
+// y-wall rows of this wave (edge tiles): D += sum_s c1(y, s) A(s), E += sum_s
+// c1 B(s) + c3 A(s) with the (wall - Toeplitz) column tables (cf. ywall8)
+template <int P, int R, int NW, int BK>
+__device__ __forceinline__ void ywall9(const StencilArgs &a, const Tile7 &t, int ybase, double (&D)[R],
+                                       double (&E)[R]) {
+  using G = Geom9<P, R, NW, BK>;
+  constexpr int W = G::W, TX = G::TX;
+  const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int y = ybase + j;
+    if (y >= yb && y < ye) {
+      double dD = 0.0, dE = 0.0;
+#pragma unroll 1
+      for (int k = 0; k < W; ++k) {
+        const int rs = y + 2 * P - k - t.y0;
+        const dpair c = ((lcdouble2 *)t.yc)[rs * W + k];
+        if constexpr (BK != 0) {
+          const dpair v = *(lcdouble2 *)(t.ab0 + G::ab(rs, t.lane));
+          dD = fma(c.x, v.x, dD);
+          dE = fma(c.x, v.y, fma(c.y, v.x, dE));
+        } else {
+          dD = fma(c.x, t.ab0[rs * TX + t.lane], dD);
+        }
+      }
+      D[j] += dD;
+      E[j] += dE;
+    }
+  }
+}
+
+template <int P, int R, int NW, int BK, int CH>
+struct Pipe9 {
+  ldouble *u[2];
+  DmaPre7<P, R, NW, NW, BK, CH> dpre;
+  XWallPre<P, BK> xpre;
+  int ybase;
+  uint32_t ocol;  // this lane's byte column x * 8, or out of range
+  // buffer stores issued between the last two DMA issues (st0) and since the
+  // last one (st1): the counted vmcnt before an x-sweep
+  int st0, st1;
+};
+
+template <int P, int R, int NW, int BK, int CH>
+__device__ __forceinline__ void dma9(const StencilArgs &a, const Tile7 &t, int zz, const Pipe9<P, R, NW, BK, CH> &pp,
+                                     int slot) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (clang's host pass rejects this instantiation; device code only)
+  stage_plane_pre7<P, R, NW, NW, BK, CH>(a, t, zz, pp.u[slot], pp.dpre);
+#endif
+}
+
+template <int P, int R, int NW, int BK, int CH>
+__device__ __forceinline__ void dma9c(const StencilArgs &a, const Tile7 &t, int zz, Pipe9<P, R, NW, BK, CH> &pp,
+                                      int slot) {
+  dma9<P, R, NW, BK, CH>(a, t, zz, pp, slot);
+  pp.st0 = pp.st1;
+  pp.st1 = 0;
+}
+
+// X(i + 1) of plane zz + 1 into AB buffer (i + 1) & 1, then DMA(i + 3) into the
+// u slot it read (waves < NG)
+template <int P, int R, int NW, int BK, int CH>
+__device__ __forceinline__ void xpart9(const StencilArgs &a, const Tile7 &t, Pipe9<P, R, NW, BK, CH> &pp, int zz) {
+  using G = Geom9<P, R, NW, BK>;
+  const int i = zz - t.zs;
+  if (zz + 1 < t.ze && t.wv < G::NG) {
+    const bool next = zz + 2 < t.ze;
+    wait_dma9<0, P, R, NW, BK, CH>(t.wv, next, next ? pp.st0 + pp.st1 : pp.st1);
+    const int s1 = (i + 1) & 1;
+    xstep9<P, R, NW, BK>(a, t, pp.u[s1], t.ab0 + s1 * G::ABSZ, pp.xpre);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (zz + 3 < t.ze) dma9c<P, R, NW, BK, CH>(a, t, zz + 3, pp, s1);
+  }
+}
+
+// stores of output plane zz - p happen in interval zz - zs when the plane is
+// in this chunk's output range
+__device__ __forceinline__ bool retires9(const Tile7 &t, int zz, int P) {
+  const int zo = zz - P;
+  return zo >= t.zc0 && zo < t.zc1;
+}
+
+template <int JP, int P, int R, int NW, int BK, int CH, int PF, bool WALL, bool YW, bool XF>
+__device__ __forceinline__ void cplane9(const StencilArgs &a, const Tile7 &t, Pipe9<P, R, NW, BK, CH> &pp,
+                                        double (&acc)[2 * P + 1][R], int zz) {
+  using G = Geom9<P, R, NW, BK>;
+  using IR = InteriorRows<P>;
+  constexpr int W = G::W;
+  const int i = zz - t.zs;
+  if (zz < t.ze) {
+    double D[R], E[R];
+    GDM_STAMPT(t, i, 0);
+    GDM_LDS_BARRIER();  // B_i: AB(i) complete
+    GDM_STAMPT(t, i, 1);
+    if constexpr (XF) xpart9<P, R, NW, BK, CH>(a, t, pp, zz);
+    Tile7 tt = t;
+    tt.ab0 = t.ab0 + (i & 1) * G::ABSZ;
+    ysweep8<P, R, NW, NW, BK, PF>(a, tt, D, E);
+    if constexpr (YW) ywall9<P, R, NW, BK>(a, tt, pp.ybase, D, E);
+    GDM_STAMPT(t, i, 2);
+    if constexpr (!WALL) {
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        GDM_FENCE();
+        const int slot = (JP - P + k + 2 * W) % W;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          if constexpr (BK == 0)
+            acc[slot][j] = fma(hcoef<P, BK>(a.zd, k), D[j], acc[slot][j]);
+          else if (zband<P, BK>(k) == 0.0)
+            acc[slot][j] = fma(IR::m[k], E[j], acc[slot][j]);
+          else
+            acc[slot][j] = fma(IR::m[k], E[j], fma(hcoef<P, BK>(a.zd, k), D[j], acc[slot][j]));
+        }
+      }
+    } else {
+      const int row = zz < W ? zz : (zz >= a.Nz - W ? W + zz - (a.Nz - W) : 2 * W);
+      lcdouble2 *zc = (lcdouble2 *)t.zt + row * W;
+      dpair cur = zc[0];
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        GDM_FENCE();
+        const dpair nxt = zc[k + 1 < W ? k + 1 : k];
+        const int slot = (JP - P + k + 2 * W) % W;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          if constexpr (BK == 0)
+            acc[slot][j] = fma(cur.y, D[j], acc[slot][j]);
+          else
+            acc[slot][j] = fma(cur.x, E[j], fma(cur.y, D[j], acc[slot][j]));
+        }
+        cur = nxt;
+      }
+    }
+  }
+  GDM_STAMPT(t, i, 3);
+#pragma unroll
+  for (int s = 0; s < W; ++s)
+#pragma unroll
+    for (int j = 0; j < R; ++j) asm volatile("" : "+v"(acc[s][j]));
+  // retire output plane zz - p: R buffer stores (lanes out of the box dropped)
+  constexpr int rslot = (JP - P + 2 * W) % W;
+  if (retires9(t, zz, P)) {
+    const int zo = zz - P;
+    const int ny_out = a.out_y1 - a.out_y0;
+    const double *plane = a.dst + (int64_t)(zo - a.out_z0) * ny_out * a.Nx;
+    __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)plane, 0, (int)((int64_t)ny_out * a.Nx * 8), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int yr = pp.ybase + j;
+      const uint32_t off = (yr < a.out_y1 && pp.ocol != 0x80000000u)
+                               ? (uint32_t)((yr - a.out_y0) * a.Nx * 8) + pp.ocol
+                               : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc[rslot][j]), rs, off, 0,
+                                            GDM_STENCIL_ST_NT ? 2 : 0);
+    }
+    pp.st1 += R;
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
+  GDM_STAMPT(t, i, 4);
+  if constexpr (!XF) xpart9<P, R, NW, BK, CH>(a, t, pp, zz);
+  GDM_STAMPT(t, i, 5);
+}
+
+template <int JP, int P, int R, int NW, int BK, int CH, int PF, bool WALL, bool YW, bool XF>
+__device__ __forceinline__ void cblock9(const StencilArgs &a, const Tile7 &t, Pipe9<P, R, NW, BK, CH> &pp,
+                                        double (&acc)[2 * P + 1][R], int zb) {
+  if constexpr (JP < 2 * P + 1) {
+    cplane9<JP, P, R, NW, BK, CH, PF, WALL, YW, XF>(a, t, pp, acc, zb + JP);
+    cblock9<JP + 1, P, R, NW, BK, CH, PF, WALL, YW, XF>(a, t, pp, acc, zb);
+  }
+}
+
+template <int P, int R, int NW, int BK, int CH, int PF, bool ZI, bool YW, bool XF>
+__device__ __forceinline__ void loop9(const StencilArgs &a, const Tile7 &t, Pipe9<P, R, NW, BK, CH> &pp) {
+  using G = Geom9<P, R, NW, BK>;
+  constexpr int W = G::W;
+  double acc[W][R];
+#pragma unroll
+  for (int s = 0; s < W; ++s)
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
+  for (int zb = t.zs; zb < t.zend; zb += W) cblock9<0, P, R, NW, BK, CH, PF, !ZI, YW, XF>(a, t, pp, acc, zb);
+}
+
+template <int P, int R, int NW, int BK, int CH, int PF, bool ZI>
+__global__ void __launch_bounds__(64 * NW, NW / 4) stencil9_kernel(StencilArgs a) {
+  using G = Geom9<P, R, NW, BK>;
+  static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget of one workgroup per CU");
+  static_assert(G::NPASS == 1, "one x-sweep row group per wave");
+  constexpr int NT = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  ldouble *lds = (ldouble *)smem;
+  Tile7 t;
+  t.u0 = lds;
+  t.ab0 = lds + G::OFF_AB;
+  t.zt = lds + G::OFF_ZT;
+  t.yc = lds + G::OFF_YC;
+  t.corr = lds + G::OFF_CORR;
+  t.yw = lds + G::OFF_YW;
+  t.lane = threadIdx.x & 63;
+  t.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  t.cw = t.wv;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (a.xcd_map) {
+    const int64_t gx = gridDim.x, gy = gridDim.y;
+    const int64_t nb = gx * gy * gridDim.z, q = nb / 8;
+    const int64_t b = blockIdx.x + gx * (blockIdx.y + gy * (int64_t)blockIdx.z);
+    const int64_t L = b >= 8 * q ? b : (b % 8) * q + b / 8;
+    bx = (int)(L % gx);
+    by = (int)((L / gx) % gy);
+    bz = (int)(L / (gx * gy));
+  }
+  t.sid = bx + gridDim.x * (by + gridDim.y * bz);
+  t.x0 = bx * G::TX;
+  t.y0 = a.out_y0 + by * G::TY;
+  t.yedge = ywall_begin<P, G::TY>(a, t.y0) >= 0;
+  {
+    const int r = bz < a.nchunk0 ? 0 : 1;
+    const int c = bz - (r ? a.nchunk0 : 0);
+    t.zc0 = a.cz0[r] + c * a.zchunk;
+    t.zc1 = min(t.zc0 + a.zchunk, a.cz1[r]);
+  }
+  t.zs = max(t.zc0 - P, a.in_z0);
+  t.ze = min(t.zc1 + P, a.in_z1);
+  t.zend = t.zc1 + P;
+  {
+    const int L = a.x_corr_left, rb = a.Nx - a.x_corr_right;
+    t.nl = max(0, min(L, t.x0 + G::TX) - t.x0);
+    t.rs = max(rb, t.x0);
+    const int nr = max(0, min(a.Nx, t.x0 + G::TX) - t.rs);
+    t.ncw = t.nl + nr;
+  }
+  if (!ZI)
+    for (int e = threadIdx.x; e < G::ZTSZ; e += NT) t.zt[e] = a.zt[e];
+  if (t.ncw > 0)
+    for (int e = threadIdx.x; e < G::CORRSZ; e += NT) t.corr[e] = a.corrX[e];
+  if (t.yedge)
+    for (int e = threadIdx.x; e < G::UR * G::W; e += NT) {
+      const int r = e / G::W, k = e - r * G::W;
+      t.yc[2 * e] = a.yT1[(size_t)(t.y0 + r) * G::W + k];
+      t.yc[2 * e + 1] = a.yT3[(size_t)(t.y0 + r) * G::W + k];
+    }
+  Pipe9<P, R, NW, BK, CH> pp;
+  pp.u[0] = t.u0;
+  pp.u[1] = t.u0 + G::USZ;
+  pp.ybase = t.y0 + t.cw * R;
+  {
+    const int x = t.x0 + t.lane;
+    pp.ocol = x < a.Nx ? (uint32_t)x * 8u : 0x80000000u;
+  }
+  pp.st0 = pp.st1 = 0;
+  const int n = t.ze - t.zs;
+  if (t.wv < G::NG) {
+    stage_pre7<P, R, NW, NW, BK, CH>(a, t, pp.dpre);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (k < n) dma9c<P, R, NW, BK, CH>(a, t, t.zs + k, pp, k);
+    if (t.ncw > 0) xwall8_pre<P, R, NW, NW, BK>(a, t, pp.xpre);
+  }
+  GDM_LDS_BARRIER();  // tables in LDS
+  if (t.wv < G::NG && n > 0) {
+    wait_dma9<0, P, R, NW, BK, CH>(t.wv, n > 1, 0);
+    xstep9<P, R, NW, BK>(a, t, pp.u[0], t.ab0, pp.xpre);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (n > 2) dma9c<P, R, NW, BK, CH>(a, t, t.zs + 2, pp, 0);
+  }
+  // odd x-sweep waves run X(i+1) before their y/z work, so every SIMD holds
+  // waves in both phases (GDM_V9_XF=0: all after)
+  const bool xf = GDM_V9_XF && (t.wv & 1) && t.wv < G::NG;
+  if (t.yedge) {
+    if (xf)
+      loop9<P, R, NW, BK, CH, PF, ZI, true, true>(a, t, pp);
+    else
+      loop9<P, R, NW, BK, CH, PF, ZI, true, false>(a, t, pp);
+  } else {
+    if (xf)
+      loop9<P, R, NW, BK, CH, PF, ZI, false, true>(a, t, pp);
+    else
+      loop9<P, R, NW, BK, CH, PF, ZI, false, false>(a, t, pp);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1485,6 +1887,44 @@ static hipError_t launch8_z(int bk, const StencilArgs &a, hipStream_t st) {
   }
 }
 
+template <int P, int R, int NW, int BK, int CH, int PF, bool ZI>
+static hipError_t launch9_t(const StencilArgs &a, hipStream_t st) {
+  using G = Geom9<P, R, NW, BK>;
+  const size_t lds = G::lds_bytes();
+  {
+    static std::atomic<uint64_t> attr_mask{0};
+    hipError_t e = gdmk_set_lds_attr((const void *)stencil9_kernel<P, R, NW, BK, CH, PF, ZI>, lds, attr_mask);
+    if (e != hipSuccess) return e;
+  }
+  int nz = 0;
+  for (int r = 0; r < 2; ++r)
+    if (a.cz1[r] > a.cz0[r]) nz += (a.cz1[r] - a.cz0[r] + a.zchunk - 1) / a.zchunk;
+  dim3 grid((a.Nx + G::TX - 1) / G::TX, (a.out_y1 - a.out_y0 + G::TY - 1) / G::TY, nz);
+  if (grid.x == 0 || grid.y == 0 || grid.z == 0) return hipSuccess;
+  hipLaunchKernelGGL((stencil9_kernel<P, R, NW, BK, CH, PF, ZI>), grid, dim3(64 * NW), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int P, int R, int NW, int PF, bool ZI>
+static hipError_t launch9_z(int bk, const StencilArgs &a, hipStream_t st) {
+  const bool vec = (a.Nx % 2 == 0) && ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0);
+  switch (bk) {
+#ifdef GDM_ONLY_ADV16
+    case 1: return vec ? launch9_t<P, R, NW, 1, 16, PF, ZI>(a, st) : hipErrorInvalidValue;
+#else
+    case 0: return vec ? launch9_t<P, R, NW, 0, 16, PF, ZI>(a, st) : launch9_t<P, R, NW, 0, 4, PF, ZI>(a, st);
+    case 1: return vec ? launch9_t<P, R, NW, 1, 16, PF, ZI>(a, st) : launch9_t<P, R, NW, 1, 4, PF, ZI>(a, st);
+    case 2: return vec ? launch9_t<P, R, NW, 2, 16, PF, ZI>(a, st) : launch9_t<P, R, NW, 2, 4, PF, ZI>(a, st);
+#endif
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int P, int R, int NW, int PF>
+static hipError_t launch9_p(int bk, bool zint, const StencilArgs &a, hipStream_t st) {
+  return zint ? launch9_z<P, R, NW, PF, true>(bk, a, st) : launch9_z<P, R, NW, PF, false>(bk, a, st);
+}
+
 template <int P, int R, int NC, int NP, int PF>
 static hipError_t launch8_p(int bk, bool zint, const StencilArgs &a, hipStream_t st) {
   return zint ? launch8_z<P, R, NC, NP, PF, true>(bk, a, st) : launch8_z<P, R, NC, NP, PF, false>(bk, a, st);
@@ -1502,7 +1942,11 @@ extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, bool zint, const gdmk:
     case 3: return launch8_p<3, 4, 8, 8, 3>(bk, zint, a, st);
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 5
+#ifdef GDM_V9_P5
+    case 5: return launch9_p<5, 2, 16, GDM_V9_P5>(bk, zint, a, st);
+#else
     case 5: return launch8_p<5, GDM_R5, GDM_NC5, GDM_NP5, GDM_PF5>(bk, zint, a, st);
+#endif
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 7
     case 7: return launch8_p<7, GDM_R7, GDM_NC7, GDM_NP7, GDM_PF7>(bk, zint, a, st);

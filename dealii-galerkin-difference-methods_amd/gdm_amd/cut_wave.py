@@ -362,9 +362,9 @@ class CutWaveCompositeProblem:
     def _upload(self, values, dst):
         dst[:len(values)].copy_(self._torch.from_numpy(np.ascontiguousarray(values, dtype=np.float64)))
 
-    def _accel(self, t, u0, u1):
-        """M_L^-1 (compute_rhs_L(u_L) + coupling(u_other)) for both fields"""
-        P, out = self.P, []
+    def _accel(self, t, u0, u1, out):
+        """out[L] = M_L^-1 (compute_rhs_L(u_L) + coupling(u_other)) for both fields"""
+        P = self.P
         for i, (cw, u, uo) in enumerate(((self.f[0], u0, u1), (self.f[1], u1, u0))):
             fq = gd = None
             if P["f"] is not None and cw.n_quad:
@@ -373,17 +373,10 @@ class CutWaveCompositeProblem:
             if cw.n_surface:
                 self._upload(call(P["g_domain"], cw.sx, t), self._gd[i])
                 gd = self._gd[i]
-            r = cw.new_vector()
-            cw.compute_rhs(u, fq, gd, r)
-            cw.couple(uo, r)
-            cw.mass_solve(r, r)
-            out.append(r)
+            cw.compute_rhs(u, fq, gd, out[i])
+            cw.couple(uo, out[i])
+            cw.mass_solve(out[i], out[i])
         return out
-
-    def _f(self, t, y):
-        if self.wave:
-            return [y[2], y[3]] + self._accel(t, y[0], y[1])
-        return self._accel(t, y[0], y[1])
 
     def postprocess(self, t, u, i):
         cw = self.f[i]
@@ -397,18 +390,31 @@ class CutWaveCompositeProblem:
         u = cw.new_vector()
         self._upload(call(P["exact"], cw.vertices, P["start_t"]), u)
         y = [u, u.clone()] + ([cw.new_vector(), cw.new_vector()] if self.wave else [])
+        nb = len(y)
+        # preallocated RK buffers (no allocation inside the time loop): the
+        # accumulator, the next stage and the two fields' accelerations
+        acc = [cw.new_vector() for _ in range(nb)]
+        Y = [cw.new_vector() for _ in range(nb)]
+        k = [cw.new_vector(), cw.new_vector()]
         dt = P["cfl"] * cw.h ** P["cfl_pow"]
         time = DiscreteTime(P["start_t"], P["end_t"], dt)
         rows = [(0, 0.0) + self.postprocess(0.0, y[0], 0), (0, 0.0) + self.postprocess(0.0, y[1], 1)]
         n = 0
         while not time.is_at_end() and (max_steps is None or n < max_steps):
             t0, h = time.t, time.next_step_size()
-            # TimeStepping::ExplicitRungeKutta, RK_CLASSIC_FOURTH_ORDER
-            ks = []
+            # TimeStepping::ExplicitRungeKutta, RK_CLASSIC_FOURTH_ORDER: y_new = ((y + h b_0 k_0) + h b_1 k_1)
+            # + ..., stage Y_s = y + h a_s k_(s-1) (one gdm_vec_rk_update per block and stage)
+            stage = y
             for s in range(4):
-                ys = y if s == 0 else [yb + (h * RK4_A[s - 1]) * kb for yb, kb in zip(y, ks[-1])]
-                ks.append(self._f(t0 + RK4_C[s] * h, ys))
-            y = [yb + sum((h * RK4_B[s]) * ks[s][b] for s in range(4)) for b, yb in enumerate(y)]
+                self._accel(t0 + RK4_C[s] * h, stage[0], stage[1], k)
+                ks = (stage[2], stage[3], k[0], k[1]) if self.wave else (k[0], k[1])
+                last = s == 3
+                a_next = 0.0 if last else h * RK4_A[s]
+                # u blocks first: they read the stage's v blocks before those are overwritten
+                for b in range(nb):
+                    cw.rk_update(h * RK4_B[s], ks[b], (y if s == 0 else acc)[b], (y if last else acc)[b], a_next,
+                                 None if last else y[b], None if last else Y[b])
+                stage = Y
             n += 1
             rows += [(n, t0 + h) + self.postprocess(t0 + h, y[0], 0), (n, t0 + h) + self.postprocess(t0 + h, y[1], 1)]
             time.advance()

@@ -5,7 +5,7 @@ reference-faithful cell loops in tests/test_oracle_kron.py):
   C2  2D advection p = 5, 1024^2 DoFs: compute_rhs (volume + outflow traces) and
       the exact mass inverse
   C4  3D wave p = 7, 256^3 DoFs: compute_rhs and the exact mass inverse
-  C3  3D advection p = 5, 512^3 DoFs: compute_rhs
+  C3  3D advection p = 5, 512^3 DoFs: compute_rhs and the exact mass inverse
 
 Same seeded inputs on both sides; tolerance rel-L2 1e-12 (fp64 summation
 order).  The inflow boundary data are covered at reduced size in
@@ -73,3 +73,18 @@ def test_c3_apply_full_size():
     got = y.cpu().numpy()
     del y
     assert _rel(got, m.kron_apply(_terms(m, "advection", A3), u)) < 1e-12
+
+
+def test_c3_mass_inverse_full_size():
+    """The headline config's per-stage solve (advection/problem.h:236-267):
+    the device's exact Kronecker mass inverse at 512^3, p = 5, against the
+    oracle's banded-Cholesky Kronecker inverse on the same right-hand side."""
+    g = _gdm()
+    op = g.GdmOperator(3, 5, 511, 0.0, 1.0, "advection", params=A3)
+    m = O.Mesh(3, 5, 511, 0.0, 1.0)
+    r = np.random.default_rng(9).uniform(-1, 1, m.n_dofs)
+    x = op.new_vector(local=False)
+    op.mass_solve(torch.from_numpy(r).cuda(), x)
+    got = x.cpu().numpy()
+    del x
+    assert _rel(got, m.kron_mass_inverse(r)) < 1e-12
