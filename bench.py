@@ -243,7 +243,65 @@ def c4_wave_stage(steps=10):
     }
     del prob, op, u, v
     torch.cuda.empty_cache()
+    out["per_rank_8"] = c4_rank_slab(steps)
     return out
+
+
+def c4_rank_slab(steps=10, n_ranks=8, rank=3):
+    """C4 at its named 8-GPU size, one rank's share on this GPU: the 256^2 x
+    32-plane slab of an interior rank (+ 2 x 7 ghost planes) of the reference's
+    slab partition (system.h:720-757).  Device work per stage of that rank: the
+    p = 7 wave stencil on the slab (wave/stiffness.h:151-181) and the
+    distributed exact mass inverse (truncated SPIKE: slab solve, one
+    refinement round, interface correction; wave/problem.h:457-502's solve).
+    The ghost exchanges between them are not part of this single-GPU figure
+    (2 x 7 planes x 0.5 MiB per exchange; xGMI point-to-point at N = 8)."""
+    import torch
+    from gdm_amd import GdmOperator
+
+    from gdm_amd import _capi
+
+    n, p = 255, 7
+    op = GdmOperator(3, p, n, -1.21, 1.21, "wave", n_ranks=n_ranks, rank=rank)
+    rounds = _capi.mesh_spike_rounds(op.mesh)
+    gen = torch.Generator(device="cuda").manual_seed(20251012)
+    u = torch.rand(op.n_local, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+    v = op.new_vector(False)
+    op.time_op(0, u, v, None, 3)
+    st_ms = op.time_op(0, u, v, None, steps)
+    x = op.new_vector(True)
+    r = v.clone()
+
+    def solve():
+        op.mass_solve_slab(r, op.owned_view(x))
+        for k in range(rounds):
+            op.mass_solve_interface_round(x, k)
+        op.mass_solve_interface(x)
+
+    solve()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        solve()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    N = op.n_owned
+    L = op.layout
+    res = {
+        "workload": "C4 rank %d of %d: 256^2 x %d owned planes + %d + %d ghost planes, p=7 wave"
+                    % (rank, n_ranks, N // L["plane_size"], L["ghost_planes_below"], L["ghost_planes_above"]),
+        "n_dofs_rank": N,
+        "stencil_ms": st_ms,
+        "stencil_valu_frac": 210.0 * N / (st_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFS,
+        "stencil_hbm_frac": BYTES_PER_DOF * N / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "spike_solve_ms": ms,
+        "spike_rounds": rounds,
+    }
+    del op, u, v, x, r
+    torch.cuda.empty_cache()
+    return res
 
 
 def _nproc():

@@ -1337,6 +1337,12 @@ int gdm_op_set_stream(gdm_op *op, void *hip_stream) {
   return GDM_OK;
 }
 
+int gdm_op_get_stream(const gdm_op *op, void **hip_stream) {
+  if (!op || !hip_stream) return fail(GDM_ERR_ARG, "NULL argument");
+  *hip_stream = (void *)op->stream;
+  return GDM_OK;
+}
+
 int gdm_op_use_own_stream(gdm_op *op) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   op->stream = op->own_stream;
@@ -2056,7 +2062,10 @@ int gdm_cut_poisson_destroy(gdm_cut_system *S) {
 // ---------------------------------------------------------------------------
 struct gdm_cut_adv_system;
 int gdmh_cut_adv_create(int p, int n_sub, double lo, double hi, const double *level_set, const double *advection,
-                        double gamma_A, double gamma_M, gdm_cut_adv_system **out, char *err, size_t err_len);
+                        double gamma_A, double gamma_M, int composite, gdm_cut_adv_system **out, char *err,
+                        size_t err_len);
+void gdmh_cut_adv_coupling(const gdm_cut_adv_system *S, const int64_t **rp, const uint32_t **ci, const double **v,
+                           int64_t *nnz);
 void gdmh_cut_adv_info(const gdm_cut_adv_system *S, int64_t *n_dofs, int64_t *n_bc, int64_t *cells,
                        int64_t *bandwidth);
 void gdmh_cut_adv_arrays(const gdm_cut_adv_system *S, const int64_t **c_rp, const uint32_t **c_ci,
@@ -2078,11 +2087,18 @@ struct gdm_cut_advection {
   int64_t *c_rp = nullptr, *f_rp = nullptr, *zrows = nullptr, n_zrows = 0;
   uint32_t *c_ci = nullptr, *f_ci = nullptr;
   double *c_v = nullptr, *f_v = nullptr, *lband = nullptr;
+  int composite = 0;  // GDM_CUT_ADV_COMPOSITE: (II)'s inflow couples to the partner field (p_*)
+  int64_t *p_rp = nullptr;
+  uint32_t *p_ci = nullptr;
+  double *p_v = nullptr;
   std::vector<double> bc_xy;
   void release() {
     for (void *q : {(void *)c_rp, (void *)f_rp, (void *)c_ci, (void *)f_ci, (void *)c_v, (void *)f_v, (void *)lband,
-                    (void *)zrows})
+                    (void *)zrows, (void *)p_rp, (void *)p_ci, (void *)p_v})
       if (q) (void)hipFree(q);
+    p_rp = nullptr;
+    p_ci = nullptr;
+    p_v = nullptr;
     zrows = nullptr;
     c_rp = f_rp = nullptr;
     c_ci = f_ci = nullptr;
@@ -2099,14 +2115,31 @@ extern "C" {
 int gdm_cut_advection_create(int fe_degree, int n_subdivisions, double left, double right, const double *level_set,
                              const double *advection, double ghost_parameter_A, double ghost_parameter_M,
                              int device, gdm_cut_advection **out) {
+  return gdm_cut_advection_create2(fe_degree, n_subdivisions, left, right, level_set, advection, ghost_parameter_A,
+                                   ghost_parameter_M, GDM_CUT_INSIDE, 0, device, out);
+}
+
+int gdm_cut_advection_create2(int fe_degree, int n_subdivisions, double left, double right, const double *level_set,
+                              const double *advection, double ghost_parameter_A, double ghost_parameter_M,
+                              int location, int flags, int device, gdm_cut_advection **out) {
   if (!out || !level_set || !advection) return fail(GDM_ERR_ARG, "NULL argument");
   *out = nullptr;
+  if (location != GDM_CUT_INSIDE && location != GDM_CUT_OUTSIDE)
+    return fail(GDM_ERR_ARG, "location: GDM_CUT_INSIDE or GDM_CUT_OUTSIDE");
+  if (flags & ~GDM_CUT_ADV_COMPOSITE) return fail(GDM_ERR_ARG, "flags: GDM_CUT_ADV_COMPOSITE only");
   GDM_GUARD_BEGIN
   auto *c = new gdm_cut_advection();
   try {
     char err[256] = {0};
-    if (gdmh_cut_adv_create(fe_degree, n_subdivisions, left, right, level_set, advection, ghost_parameter_A,
-                            ghost_parameter_M, &c->host, err, sizeof(err)) != 0) {
+    // the outside field = the same assembly on the negated level set (its inside is the outside region;
+    // MeshClassifier, face parts, surface normal and ghost-penalty faces follow the sign)
+    const size_t nv = n_subdivisions >= 0 ? (size_t)(n_subdivisions + 1) * (size_t)(n_subdivisions + 1) : 0;
+    std::vector<double> ls(level_set, level_set + nv);
+    if (location == GDM_CUT_OUTSIDE)
+      for (double &v : ls) v = -v;
+    c->composite = (flags & GDM_CUT_ADV_COMPOSITE) != 0;
+    if (gdmh_cut_adv_create(fe_degree, n_subdivisions, left, right, ls.data(), advection, ghost_parameter_A,
+                            ghost_parameter_M, c->composite, &c->host, err, sizeof(err)) != 0) {
       delete c;
       return fail(GDM_ERR_ARG, err);
     }
@@ -2145,6 +2178,16 @@ int gdm_cut_advection_create(int fe_degree, int n_subdivisions, double left, dou
     gdmh_cut_adv_zero_rows(c->host, &zr, &c->n_zrows);
     if (c->n_zrows > 0) c->zrows = dev_upload(std::vector<int64_t>(zr, zr + c->n_zrows));
     c->bc_xy.assign(xy, xy + 2 * c->n_bc);
+    if (c->composite) {
+      const int64_t *prp;
+      const uint32_t *pci;
+      const double *pv;
+      int64_t pnnz = 0;
+      gdmh_cut_adv_coupling(c->host, &prp, &pci, &pv, &pnnz);
+      c->p_rp = dev_upload(std::vector<int64_t>(prp, prp + N + 1));
+      c->p_ci = dev_upload(std::vector<uint32_t>(pci, pci + std::max<int64_t>(pnnz, 1)));
+      c->p_v = dev_upload(std::vector<double>(pv, pv + std::max<int64_t>(pnnz, 1)));
+    }
   } catch (...) {
     c->release();
     delete c;
@@ -2188,6 +2231,17 @@ int gdm_cut_advection_compute_rhs(gdm_cut_advection *c, const double *u, const d
   hip_check(gdmk_launch_csr_accum(c->n_dofs, c->c_rp, c->c_ci, c->c_v, u, rhs, c->op->stream), "cut correction");
   if (c->n_bc > 0)
     hip_check(gdmk_launch_csr_accum(c->n_dofs, c->f_rp, c->f_ci, c->f_v, bc, rhs, c->op->stream), "inflow data");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_cut_advection_couple(gdm_cut_advection *c, const double *u_partner, double *rhs) {
+  if (!c || !u_partner || !rhs) return fail(GDM_ERR_ARG, "NULL argument");
+  if (!c->composite) return fail(GDM_ERR_STATE, "gdm_cut_advection_couple: created without GDM_CUT_ADV_COMPOSITE");
+  if (u_partner == rhs) return fail(GDM_ERR_ARG, "u_partner and rhs must be distinct");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(c->op->device), "hipSetDevice");
+  hip_check(gdmk_launch_csr_accum(c->n_dofs, c->p_rp, c->p_ci, c->p_v, u_partner, rhs, c->op->stream), "coupling");
   return GDM_OK;
   GDM_GUARD_END
 }

@@ -1,7 +1,13 @@
 // gdm_cut_advection.cpp -- host assembly of the cut-cell parts of the 2D
-// advection application (applications/advection, non-composite, alpha = 0)
-// for the device operator of gdm_capi.cpp ("Cut-cell advection" in
-// include/gdm_hip.h).
+// advection application (applications/advection, alpha = 0) for the device
+// operator of gdm_capi.cpp ("Cut-cell advection" in include/gdm_hip.h).
+// Composite (advection-app.cc's preset, problem.h:103-181): one system per
+// field; the outside field is this assembly on the negated level set (its
+// inside = the outside of the level set, the surface normal flipped as in
+// stiffness.h:437, the ghost-penalty faces and the mass of
+// MassMatrixOperator(location = outside)), and the inflow value u+ of the
+// cut-surface term (II) is the partner field (stiffness.h:448-453): a
+// coupling matrix P instead of stage boundary points.
 //
 // The device evaluates compute_rhs (advection/stiffness.h:196-606) as
 //   rhs = Z (S u) + C u + F bc
@@ -47,6 +53,7 @@
 
 struct gdm_cut_adv_system {
   int p = 0, n = 0;
+  bool composite = false;  // (II)'s inflow value is the partner field's u (coupling P), not stage data
   double lo = 0.0, h = 0.0, a[2] = {0.0, 0.0}, gA = 0.0, gM = 0.0;
   std::vector<double> ls;   // vertex level set [iy][ix]
   std::vector<int8_t> loc;  // [cy][cx]
@@ -61,6 +68,9 @@ struct gdm_cut_adv_system {
   std::vector<int64_t> m_rp;  // the assembled cut mass matrix (host checks)
   std::vector<uint32_t> m_ci;
   std::vector<double> m_v;
+  std::vector<int64_t> p_rp;  // composite: the partner coupling of (II), rhs += P u_partner
+  std::vector<uint32_t> p_ci;
+  std::vector<double> p_v;
 };
 
 namespace {
@@ -117,9 +127,10 @@ void assemble(gdm_cut_adv_system &S) {
   const double h = S.h, ax = S.a[0], ay = S.a[1];
   std::vector<double> qx, qw;
   gauss_unit(n1, qx, qw);
-  SlotMatrix C, M;
+  SlotMatrix C, M, Pc;
   C.init(N, p + 1);
   M.init(N, p + 1);
+  if (S.composite) Pc.init(N, p + 1);
   struct FEntry {
     int64_t row, col;
     double v;
@@ -241,9 +252,19 @@ void assemble(gdm_cut_adv_system &S) {
           saye_unit(fl, qx, qw, ins, sur);
           volume(ins, 1.0, true);
           for (const SPoint &q : sur) {  // (II) cut surface
-            add_point(q.s, q.t);
-            upwind(q.s, q.t, q.nx * ax + q.ny * ay, q.w * h, 1.0, true);
-            ++n_bc;
+            const double flux = q.nx * ax + q.ny * ay;
+            if (S.composite) {
+              // u+ = the partner field at the point (stiffness.h:448-453): the inflow part couples to its
+              // DoFs through this cell's basis, no stage boundary point (collect_boundary_points :115)
+              upwind(q.s, q.t, flux, q.w * h, 1.0, false);
+              if (flux < 0.0)
+                for (int i = 0; i < nd; ++i)
+                  for (int j = 0; j < nd; ++j) Pc.add(d[i], d[j], -flux * val[i] * val[j] * q.w * h);
+            } else {
+              add_point(q.s, q.t);
+              upwind(q.s, q.t, flux, q.w * h, 1.0, true);
+              ++n_bc;
+            }
           }
         }
         for (int f = 0; f < 4; ++f) {  // (III) box faces: outflow into K, inflow into F
@@ -300,6 +321,7 @@ void assemble(gdm_cut_adv_system &S) {
     }
   C.csr(S.c_rp, S.c_ci, S.c_v, false);
   M.csr(S.m_rp, S.m_ci, S.m_v, true);
+  if (S.composite) Pc.csr(S.p_rp, S.p_ci, S.p_v, false);
   // F: CSR rows = DoFs, columns = boundary points (ascending point index)
   std::sort(fent.begin(), fent.end(), [](const FEntry &x, const FEntry &y) {
     return x.row != y.row ? x.row < y.row : x.col < y.col;
@@ -356,7 +378,8 @@ void assemble(gdm_cut_adv_system &S) {
 extern "C" {
 
 int gdmh_cut_adv_create(int p, int n_sub, double lo, double hi, const double *level_set, const double *advection,
-                        double gamma_A, double gamma_M, gdm_cut_adv_system **out, char *err, size_t err_len) {
+                        double gamma_A, double gamma_M, int composite, gdm_cut_adv_system **out, char *err,
+                        size_t err_len) {
   try {
     if (!out || !level_set || !advection || p < 1 || p > 9 || p % 2 == 0 || n_sub < p || !(hi > lo))
       throw std::invalid_argument("cut_advection: invalid arguments (p odd in [1, 9], n_sub >= p, hi > lo)");
@@ -371,6 +394,7 @@ int gdmh_cut_adv_create(int p, int n_sub, double lo, double hi, const double *le
     S->a[1] = advection[1];
     S->gA = gamma_A;
     S->gM = gamma_M;
+    S->composite = composite != 0;
     const int N = n_sub + 1;
     S->ls.assign(level_set, level_set + (size_t)N * N);
     S->loc.resize((size_t)n_sub * n_sub);
@@ -431,6 +455,15 @@ void gdmh_cut_adv_mass(const gdm_cut_adv_system *S, const int64_t **rp, const ui
   *rp = S->m_rp.data();
   *ci = S->m_ci.data();
   *v = S->m_v.data();
+}
+
+// composite: rhs += P u_partner (rows = DoFs, columns = the partner's DoFs); empty otherwise
+void gdmh_cut_adv_coupling(const gdm_cut_adv_system *S, const int64_t **rp, const uint32_t **ci, const double **v,
+                           int64_t *nnz) {
+  *rp = S->p_rp.data();
+  *ci = S->p_ci.data();
+  *v = S->p_v.data();
+  *nnz = S->p_rp.empty() ? 0 : S->p_rp.back();
 }
 
 void gdmh_cut_adv_destroy(gdm_cut_adv_system *S) { delete S; }

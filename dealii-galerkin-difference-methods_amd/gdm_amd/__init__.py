@@ -9,9 +9,9 @@ from ._capi import GdmError, load, declared_symbols, device_count  # noqa: F401
 from .operator import GdmOperator  # noqa: F401
 from .sparse import CutPoisson, SparseMatrix, solve_cg  # noqa: F401
 from .problem import Advection01, AdvectionProblem, DiscreteTime, WaveProblem  # noqa: F401
-from .cut_advection import CutAdvection, CutAdvectionProblem  # noqa: F401
+from .cut_advection import CutAdvection, CutAdvectionCompositeProblem, CutAdvectionProblem  # noqa: F401
 from .cut_wave import CutWave, CutWaveCompositeProblem, CutWaveProblem  # noqa: F401
 
 __all__ = ["GdmError", "GdmOperator", "SparseMatrix", "CutPoisson", "solve_cg", "load", "declared_symbols", "device_count",
-           "Advection01", "AdvectionProblem", "WaveProblem", "DiscreteTime", "CutAdvection", "CutAdvectionProblem",
+           "Advection01", "AdvectionProblem", "WaveProblem", "DiscreteTime", "CutAdvection", "CutAdvectionProblem", "CutAdvectionCompositeProblem",
            "CutWave", "CutWaveProblem", "CutWaveCompositeProblem"]

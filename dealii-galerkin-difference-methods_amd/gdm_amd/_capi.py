@@ -124,6 +124,7 @@ def load():
         "gdm_vec_pointwise_mult": [P, i64, P, P, P],
         "gdm_op_set_stream": [P, P],
         "gdm_op_use_own_stream": [P],
+        "gdm_op_get_stream": [P, P],
         "gdm_apply": [P, P, P, P],
         "gdm_add_boundary_data": [P, P, P],
         "gdm_apply_planes": [P, P, P, i32, i32],
@@ -175,6 +176,8 @@ def load():
         "gdm_cut_advection_op": [P, ctypes.POINTER(P)],
         "gdm_cut_advection_compute_rhs": [P, P, P, P],
         "gdm_cut_advection_mass_solve": [P, P, P],
+        "gdm_cut_advection_create2": [i32, i32, d, d, P, P, d, d, i32, i32, i32, ctypes.POINTER(P)],
+        "gdm_cut_advection_couple": [P, P, P],
         "gdm_cut_advection_destroy": [P],
         "gdm_cut_wave_create": [i32, i32, i32, d, d, i32, P, i32, i32, d, d, d, i32, ctypes.POINTER(P)],
         "gdm_cut_wave_info": [P, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64), P],

@@ -8,6 +8,12 @@ entry points of include/gdm_hip.h.
                        of the box (cut rows zeroed) + host-assembled cut rows + inflow
                        data, and the mass solve (mass.h:47-243 +
                        problem.h:236-267) as an exact banded solve
+  CutAdvectionCompositeProblem
+                       AdvectionProblem::run, composite branch (problem.h:103-181,
+                       advection-app.cc's preset): an inside and an outside
+                       field, each with its own advection, region, ghost
+                       penalty and mass; the cut-surface inflow value is the
+                       partner field (stiffness.h:448-453)
   CutAdvectionProblem  AdvectionProblem::run (problem.h:31-102): DiscreteTime,
                        initialize_time_step (block(0) = g(t_n) at the stage
                        boundary points), RK_CLASSIC_FOURTH_ORDER with
@@ -39,10 +45,16 @@ class CutAdvection:
     """Device operator of the cut advection problem on [left, right]^2.
 
     level_set: callable f(x, y) (vectorised) or the (n+1)^2 vertex values
-    (x fastest); its FE_Q(1) interpolant defines inside (< 0)."""
+    (x fastest); its FE_Q(1) interpolant defines inside (< 0).
+    location: INSIDE (the field on phi < 0) or OUTSIDE (phi > 0); composite:
+    the cut-surface inflow value is a partner field (couple()) instead of stage
+    boundary data (include/gdm_hip.h gdm_cut_advection_create2)."""
+
+    INSIDE, OUTSIDE = -1, 1  # GDM_CUT_INSIDE / GDM_CUT_OUTSIDE
+    COMPOSITE = 1            # GDM_CUT_ADV_COMPOSITE
 
     def __init__(self, fe_degree, n_subdivisions, left, right, level_set, advection, ghost_parameter_A=0.5,
-                 ghost_parameter_M=0.5, device=0):
+                 ghost_parameter_M=0.5, device=0, location=-1, composite=False):
         self._lib = _capi.load()
         self._h = ctypes.c_void_p()
         N = n_subdivisions + 1
@@ -56,10 +68,13 @@ class CutAdvection:
         if ls.shape[0] != N * N:
             raise GdmError("level_set: %d vertex values expected" % (N * N))
         a = (ctypes.c_double * 2)(*[float(v) for v in advection])
-        check(self._lib.gdm_cut_advection_create(int(fe_degree), int(n_subdivisions), float(left), float(right),
-                                                 ls.ctypes.data_as(ctypes.c_void_p), a, float(ghost_parameter_A),
-                                                 float(ghost_parameter_M), int(device), ctypes.byref(self._h)),
-              "gdm_cut_advection_create")
+        self.location, self.composite = int(location), bool(composite)
+        check(self._lib.gdm_cut_advection_create2(int(fe_degree), int(n_subdivisions), float(left), float(right),
+                                                  ls.ctypes.data_as(ctypes.c_void_p), a, float(ghost_parameter_A),
+                                                  float(ghost_parameter_M), self.location,
+                                                  self.COMPOSITE if composite else 0, int(device),
+                                                  ctypes.byref(self._h)),
+              "gdm_cut_advection_create2")
         nd, nb, bw = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         cells = (ctypes.c_int64 * 3)()
         check(self._lib.gdm_cut_advection_info(self._h, ctypes.byref(nd), ctypes.byref(nb), cells, ctypes.byref(bw)),
@@ -104,6 +119,11 @@ class CutAdvection:
     def compute_rhs(self, u, bc, out):
         check(self._lib.gdm_cut_advection_compute_rhs(self._h, _ptr(u), _ptr(bc) if self.n_bc_points else None,
                                                       _ptr(out)), "gdm_cut_advection_compute_rhs")
+        return out
+
+    def couple(self, u_partner, out):
+        """out += P u_partner: the partner field's inflow on the cut surface (composite)"""
+        check(self._lib.gdm_cut_advection_couple(self._h, _ptr(u_partner), _ptr(out)), "gdm_cut_advection_couple")
         return out
 
     def mass_solve(self, rhs, x):
@@ -175,4 +195,82 @@ class CutAdvectionProblem:
             n += 1
             time.advance()
         self.ca.synchronize()
+        return n
+
+
+class CutAdvectionCompositeProblem:
+    """AdvectionProblem::run, composite branch (problem.h:103-181) on the
+    device: BlockVector (bc_in, u_in, bc_out, u_out), f = (dg/dt,
+    M_in^-1 (rhs_in(u_in, bc_in) + P_in u_out), dg/dt, M_out^-1 (rhs_out +
+    P_out u_in)), RK_CLASSIC_FOURTH_ORDER in the low-storage form (deal.II's
+    summation order), both fields on one stream.  exact / exact_dt: g and
+    dg/dt (vectorised numpy) at the stage boundary points of each field.
+    The reference prints nothing for this preset (advection-app.cc), so the
+    device run is checked against oracle/cut_advection2d.py's restatement:
+    parity unpinned."""
+
+    def __init__(self, p, n_sub, left, right, level_set, advection_in, advection_out, exact, exact_dt,
+                 ghost_parameter_A=0.5, ghost_parameter_M=0.5, device=0):
+        import torch
+
+        self.f = [CutAdvection(p, n_sub, left, right, level_set, adv, ghost_parameter_A, ghost_parameter_M, device,
+                               location=loc, composite=True)
+                  for loc, adv in ((CutAdvection.INSIDE, advection_in), (CutAdvection.OUTSIDE, advection_out))]
+        # one stream for both fields (the coupling reads the partner's stage)
+        s = torch.cuda.current_stream(device).cuda_stream
+        for ca in self.f:
+            check(ca._lib.gdm_op_set_stream(ca._op, ctypes.c_void_p(s)), "gdm_op_set_stream")
+        self.g, self.dg, self._torch = exact, exact_dt, torch
+        self.pts = [ca.bc_points() for ca in self.f]
+        nb = [max(ca.n_bc_points, 1) for ca in self.f]
+        ca = self.f[0]
+        sizes = [nb[0], ca.n_dofs, nb[1], ca.n_dofs]
+        self.y = [ca.new_vector(n) for n in sizes]
+        self._acc = [ca.new_vector(n) for n in sizes]
+        self._Y = [ca.new_vector(n) for n in sizes]
+        self._k = [ca.new_vector(n) for n in sizes]
+
+    def _upload(self, values, dst):
+        dst[:len(values)].copy_(self._torch.from_numpy(np.ascontiguousarray(values, dtype=np.float64)))
+
+    def set_initial_condition(self, t=0.0):
+        X, Y = np.meshgrid(self.f[0].vertices, self.f[0].vertices, indexing="xy")
+        u0 = self.g(X.reshape(-1), Y.reshape(-1), t)
+        self._upload(u0, self.y[1])
+        self._upload(u0, self.y[3])
+
+    def _rhs(self, t, stage, k):
+        for i, (ca, pts) in enumerate(zip(self.f, self.pts)):
+            bb, ub = 2 * i, 2 * i + 1
+            if ca.n_bc_points:
+                self._upload(self.dg(pts[:, 0], pts[:, 1], t), k[bb])
+            ca.compute_rhs(stage[ub], stage[bb], k[ub])
+            ca.couple(stage[3 - 2 * i], k[ub])  # the partner field's u
+            ca.mass_solve(k[ub], k[ub])
+
+    def step(self, t, h):
+        y, acc, Y, k = self.y, self._acc, self._Y, self._k
+        for i, (ca, pts) in enumerate(zip(self.f, self.pts)):  # initialize_time_step
+            if ca.n_bc_points:
+                self._upload(self.g(pts[:, 0], pts[:, 1], t), y[2 * i])
+        stage = y
+        ca = self.f[0]
+        for s in range(4):
+            self._rhs(t + RK4_C[s] * h, stage, k)
+            last = s == 3
+            a_next = 0.0 if last else h * RK4_A[s]
+            for b in range(4):
+                ca.rk_update(h * RK4_B[s], k[b], (y if s == 0 else acc)[b], (y if last else acc)[b], a_next,
+                             None if last else y[b], None if last else Y[b])
+            stage = Y
+
+    def run(self, start_t, end_t, dt, max_steps=None):
+        self.set_initial_condition(start_t)
+        time = DiscreteTime(start_t, end_t, dt)
+        n = 0
+        while not time.is_at_end() and (max_steps is None or n < max_steps):
+            self.step(time.t, time.next_step_size())
+            n += 1
+            time.advance()
+        self.f[0].synchronize()
         return n

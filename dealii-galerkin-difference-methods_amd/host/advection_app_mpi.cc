@@ -6,7 +6,10 @@
 //
 //   mpirun -np R advection_app_mpi DIM P N STEPS CFL OUT [DEVBC] [COMM]
 //
-// COMM = mpi (default) | rccl.  Rank r uses device r % n_devices.  Same
+// COMM = mpi (default) | rccl, each optionally suffixed -blocking (exchange,
+// then apply; default: the exchange overlapped with the interior planes,
+// StiffnessMatrixOperator::compute_rhs_overlapped).  Rank r uses device
+// r % n_devices.  Same
 // manufactured solution, output and printed lines as advection_app; OUT holds
 // the ranks' owned values in rank order (gathered on rank 0).
 #include <gdm/hip/mpi_communicator.h>
@@ -79,6 +82,12 @@ int run(int p, int n, int steps, double cfl, const char *out, int devbc, const s
   }
   params.n_ranks = size;
   params.rank = rank;
+  const std::string blk = "-blocking";
+  std::string kind = comm_kind;
+  if (kind.size() > blk.size() && kind.compare(kind.size() - blk.size(), blk.size(), blk) == 0) {
+    params.overlap_exchange = false;
+    kind = kind.substr(0, kind.size() - blk.size());
+  }
   gdm_mesh_desc mesh{};
   mesh.dim = dim;
   mesh.fe_degree = p;
@@ -89,7 +98,7 @@ int run(int p, int n, int steps, double cfl, const char *out, int devbc, const s
   }
   mesh.n_ranks = size;
   std::unique_ptr<GDM::HIP::Communicator> comm;
-  if (comm_kind == "rccl") {
+  if (kind == "rccl") {
 #ifdef GDM_WITH_RCCL
     comm = std::make_unique<GDM::HIP::RcclRank>(MPI_COMM_WORLD, mesh, device);
 #else
@@ -121,8 +130,8 @@ int run(int p, int n, int steps, double cfl, const char *out, int devbc, const s
   double s = 0.0;
   for (double v : u) s += v * v;
   std::printf("steps %u  |u|_2 %.15e\n", done, std::sqrt(s));
-  std::printf("mass solve: %s, comm: %s, ranks %d\n", problem.used_spike_solve() ? "spike" : "cg", comm_kind.c_str(),
-              size);
+  std::printf("mass solve: %s, comm: %s, ranks %d, exchange %s\n", problem.used_spike_solve() ? "spike" : "cg",
+              kind.c_str(), size, params.overlap_exchange ? "overlapped" : "blocking");
   if (devbc) std::printf("%5d %8.5f %14.8e %14.8e %14.8e\n", 0, time_of(done, n, cfl), norms[2], norms[1], norms[0]);
   std::ofstream f(out, std::ios::binary);
   f.write(reinterpret_cast<const char *>(u.data()), sizeof(double) * u.size());
@@ -135,7 +144,7 @@ int main(int argc, char **argv) {
   MPI_Init(&argc, &argv);
   int rc = 2;
   if (argc < 7) {
-    std::fprintf(stderr, "usage: %s DIM P N STEPS CFL OUT [DEVBC] [mpi|rccl]\n", argv[0]);
+    std::fprintf(stderr, "usage: %s DIM P N STEPS CFL OUT [DEVBC] [mpi|rccl][-blocking]\n", argv[0]);
   } else {
     const int dim = std::atoi(argv[1]), p = std::atoi(argv[2]), n = std::atoi(argv[3]), steps = std::atoi(argv[4]);
     const double cfl = std::atof(argv[5]);

@@ -62,6 +62,9 @@ struct Parameters {
   std::array<double, dim> advection{};  // constant field a
   int device = 0;
   int n_ranks = 1, rank = 0;            // z-slab partition (system.h:720-757)
+  // n_ranks > 1: overlap the stage's ghost exchange with the interior planes
+  // (Communicator::begin_ / end_update_ghost_values); false: exchange, then apply
+  bool overlap_exchange = true;
   // Device evaluation of g / dg/dt at the boundary points (gdm_eval_boundary):
   // a gdm_fn_kind (GDM_FN_CONE = the advection app's ExactSolution,
   // advection-app.cc:51-79; GDM_FN_SINE_PRODUCT = a transported product of
@@ -169,6 +172,17 @@ class Communicator {
   virtual ~Communicator() = default;
   // fill the ghost planes of `local` (engine-local layout of `op`) from the slab neighbours
   virtual void update_ghost_values(gdm_op *op, DeviceVector &local) = 0;
+  // Split-phase form, for overlapping the exchange with work that reads no
+  // ghost plane (the interior planes of the stencil, advection/stiffness.h:343
+  // update_ghost_values before the cell loop): begin_ starts the exchange once
+  // the owned planes queued on `op` are final; after end_ the ghost planes are
+  // visible to everything queued on `op` later.  The default runs the whole
+  // exchange in begin_.
+  virtual void begin_update_ghost_values(gdm_op *op, DeviceVector &local) { update_ghost_values(op, local); }
+  virtual void end_update_ghost_values(gdm_op *op, DeviceVector &local) {
+    (void)op;
+    (void)local;
+  }
   virtual double sum(double local_value) = 0;
   // Utilities::MPI::max (the Linf reduction of the postprocess, problem.h:410-411)
   virtual double max(double local_value) = 0;
@@ -264,6 +278,36 @@ class StiffnessMatrixOperator {
     check(gdm_apply(op, stage_bc_and_solution.block(1).get_values(), owned(vec_rhs.block(1)),
                     stage_bc_and_solution.block(0).get_values()),
           "gdm_apply");
+  }
+
+  // compute_rhs of one slab rank with the ghost exchange of `src`'s block(1)
+  // overlapped (stiffness.h:343 + :345-605): the output planes whose 2p+1
+  // input planes are all owned run while the exchange is in flight, the p
+  // planes next to each slab edge after it, then the inflow boundary data.
+  // Same additions in the same order as update_ghost_values + compute_rhs.
+  // Plane ranges exist in 3D (gdm_apply_planes); other dims exchange first.
+  void compute_rhs_overlapped(BlockVector &vec_rhs, BlockVector &src, const double time, Communicator &comm) const {
+    if (dim != 3) {
+      comm.update_ghost_values(op, src.block(1));
+      compute_rhs(vec_rhs, src, time);
+      return;
+    }
+    set_boundary(vec_rhs.block(0), time, 1);
+    const int p = layout.halo_depth, pb = (int)layout.owned_plane_begin, pe = (int)layout.owned_plane_end;
+    const int lo = pb + (layout.ghost_planes_below ? p : 0), hi = pe - (layout.ghost_planes_above ? p : 0);
+    const double *u = src.block(1).get_values();
+    double *dst = owned(vec_rhs.block(1));
+    comm.begin_update_ghost_values(op, src.block(1));
+    if (hi > lo) check(gdm_apply_planes(op, u, dst, lo, hi), "gdm_apply_planes");
+    comm.end_update_ghost_values(op, src.block(1));
+    if (hi <= lo) {
+      check(gdm_apply_planes(op, u, dst, pb, pe), "gdm_apply_planes");
+    } else {
+      if (lo > pb) check(gdm_apply_planes(op, u, dst, pb, lo), "gdm_apply_planes");
+      if (pe > hi) check(gdm_apply_planes(op, u, dst, hi, pe), "gdm_apply_planes");
+    }
+    if (layout.n_bc_points > 0)
+      check(gdm_add_boundary_data(op, src.block(0).get_values(), dst), "gdm_add_boundary_data");
   }
 
   gdm_op *handle() const { return op; }
@@ -483,8 +527,12 @@ class AdvectionProblem {
     if (params.n_ranks != 1) rhs_tmp.reinit(stiffness_matrix_operator.handle(), stiffness_matrix_operator.get_layout().n_owned);
     use_spike = params.n_ranks != 1 && mass_matrix_operator.spike_available();
     const auto fu_rhs = [&](double time, BlockVector &y, BlockVector &result) {
-      if (params.n_ranks != 1) comm->update_ghost_values(stiffness_matrix_operator.handle(), y.block(1));
-      stiffness_matrix_operator.compute_rhs(result, y, time);
+      if (params.n_ranks != 1 && params.overlap_exchange) {
+        stiffness_matrix_operator.compute_rhs_overlapped(result, y, time, *comm);
+      } else {
+        if (params.n_ranks != 1) comm->update_ghost_values(stiffness_matrix_operator.handle(), y.block(1));
+        stiffness_matrix_operator.compute_rhs(result, y, time);
+      }
       double *r = stiffness_matrix_operator.owned(result.block(1));
       if (params.n_ranks == 1) {
         mass_matrix_operator.solve(r, r);

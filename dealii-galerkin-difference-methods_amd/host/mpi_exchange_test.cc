@@ -7,7 +7,8 @@
 // Every rank fills its owned entries with their global DoF index, exchanges
 // the ghost planes and checks that each received entry holds the global index
 // of the vertex it stands for (the lower neighbour's last planes below, the
-// upper neighbour's first planes above), then checks MPI sum / max.  Prints
+// upper neighbour's first planes above), repeats the exchange in split phase
+// (post, work, wait) and compares bitwise, then checks MPI sum / max.  Prints
 // "ok" on rank 0.
 #include <gdm/hip/mpi_communicator.h>
 #include <mpi.h>
@@ -51,6 +52,19 @@ int main(int argc, char **argv) {
     for (int64_t i = 0; i < plan.recv_above_count; ++i)
       bad += local[plan.recv_above_offset + i] != (double)(g0 + owned + i);
     if ((rank > 0) != (plan.recv_below_count > 0) || (rank + 1 < size && pe <= n) != (plan.recv_above_count > 0)) ++bad;
+    // split phase (MpiRank::begin_ / end_update_ghost_values): post, work on
+    // the owned interior meanwhile, wait -- the same ghost entries, bit for bit
+    std::vector<double> split(local.size(), -1.0);
+    for (int64_t i = 0; i < owned; ++i) split[plan.owned_offset + i] = (double)(g0 + i);
+    GDM::HIP::PlaneRequests req;
+    GDM::HIP::post_planes(plan, MPI_COMM_WORLD, split.data() + plan.send_below_offset,
+                          split.data() + plan.send_above_offset, split.data() + plan.recv_below_offset,
+                          split.data() + plan.recv_above_offset, req);
+    double interior = 0.0;
+    for (int64_t i = 0; i < owned; ++i) interior += split[plan.owned_offset + i];
+    req.wait();
+    bad += interior != interior;  // (keeps the overlapped work)
+    for (std::size_t i = 0; i < local.size(); ++i) bad += split[i] != local[i];
     GDM::HIP::MpiRank comm(MPI_COMM_WORLD, mesh);
     const double s = comm.sum(rank + 1.0), m = comm.max(rank + 0.5);
     bad += s != size * (size + 1) / 2.0;

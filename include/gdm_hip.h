@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 9
+#define GDM_HIP_ABI_VERSION 10
 
 enum gdm_status {
   GDM_OK = 0,
@@ -164,6 +164,11 @@ int gdm_op_layout(const gdm_op *op, gdm_layout *out);
  * private non-blocking stream */
 int gdm_op_set_stream(gdm_op *op, void *hip_stream);
 int gdm_op_use_own_stream(gdm_op *op);
+/* the hipStream_t the operator launches on now (set or own): a communicator
+ * orders a device-side ghost exchange after the operator's work on it and
+ * makes later work wait for the exchange (RcclRank's split-phase
+ * update_ghost_values, advection/stiffness.h:343) -- ABI v10 */
+int gdm_op_get_stream(const gdm_op *op, void **hip_stream);
 
 /* dst_owned = K src_local (+ inflow boundary-data term when bc_values != NULL,
  * advection only: bc_values are the stage boundary values, device order, size
@@ -462,6 +467,24 @@ int gdm_cut_advection_op(gdm_cut_advection *c, gdm_op **op);
 int gdm_cut_advection_compute_rhs(gdm_cut_advection *c, const double *u, const double *bc, double *rhs);
 int gdm_cut_advection_mass_solve(gdm_cut_advection *c, const double *rhs, double *x);
 int gdm_cut_advection_destroy(gdm_cut_advection *c);
+/* Composite advection (advection-app.cc's preset: params.composite, problem.h
+ * :103-181; ABI v10): one handle per field.  location GDM_CUT_INSIDE (phi < 0,
+ * params.advection) or GDM_CUT_OUTSIDE (phi > 0, params.advection_1; the
+ * region, its box-face parts, the surface normal (stiffness.h:437), the ghost
+ * penalty and the mass of MassMatrixOperator(location) follow the sign).
+ * flags GDM_CUT_ADV_COMPOSITE: the inflow value u+ of the cut-surface term (II)
+ * is the partner field evaluated at the surface point (stiffness.h:448-453),
+ * so the surface points are no stage boundary points (collect_boundary_points
+ * :115) and gdm_cut_advection_couple adds that part: rhs += P u_partner
+ * (u_partner: the other field's DoF vector, same numbering).  compute_rhs(u,
+ * bc, rhs) + couple(u_partner, rhs) = the field's block of compute_rhs
+ * (stiffness.h:196-214); the box-face inflow (III) still reads bc.
+ * gdm_cut_advection_create = create2(..., GDM_CUT_INSIDE, 0, ...). */
+#define GDM_CUT_ADV_COMPOSITE 1
+int gdm_cut_advection_create2(int fe_degree, int n_subdivisions, double left, double right, const double *level_set,
+                              const double *advection /* [2] */, double ghost_parameter_A, double ghost_parameter_M,
+                              int location, int flags, int device, gdm_cut_advection **out);
+int gdm_cut_advection_couple(gdm_cut_advection *c, const double *u_partner, double *rhs);
 
 /* ------------------------------------------------------------------------
  * Cut-cell wave / heat / poisson (applications/wave, location

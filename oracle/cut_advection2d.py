@@ -161,6 +161,8 @@ class CutAdvection2D:
         Kr, Kc, Kv = [], [], []
         Mr, Mc, Mv = [], [], []
         Fr, Fc, Fv = [], [], []
+        Pr, Pc, Pv = [], [], []  # composite: (II)'s inflow from the partner field
+        composite = getattr(self, "composite", False)
         pts = []  # boundary points (x, y) in the reference's point_counter order
 
         def add(R, C, V, rows, cols, mat):
@@ -196,9 +198,18 @@ class CutAdvection2D:
                     w = np.array([c[2] for c in sur])
                     nr = np.array([c[3] for c in sur])
                     val, _ = g.shapes(cx, cy, s, t)
-                    for q in range(len(w)):
-                        pts.append(g.real_point(cx, cy, s[q], t[q]))
-                    upwind(d, val, nr @ self.a, w)
+                    if composite:
+                        # u+ = the partner field at the point (stiffness.h:448-453); no stage point (:115)
+                        flux = nr @ self.a
+                        for q in range(len(w)):
+                            if flux[q] >= 0.0:
+                                add(Kr, Kc, Kv, d, d, -flux[q] * w[q] * np.outer(val[:, q], val[:, q]))
+                            else:
+                                add(Pr, Pc, Pv, d, d, -flux[q] * w[q] * np.outer(val[:, q], val[:, q]))
+                    else:
+                        for q in range(len(w)):
+                            pts.append(g.real_point(cx, cy, s[q], t[q]))
+                        upwind(d, val, nr @ self.a, w)
                 for f in range(4):  # (III) box faces
                     at_bnd = (f == 0 and cx == 0) or (f == 1 and cx == n - 1) or (f == 2 and cy == 0) or \
                              (f == 3 and cy == n - 1)
@@ -234,6 +245,7 @@ class CutAdvection2D:
         Mc = self.M.tocsr()
         Mc.sort_indices()
         self._csr = (Mc.indptr.astype(np.int64), Mc.indices.astype(np.int64), Mc.data)
+        self.P = sps.csr_matrix((cat(Pv), (cat(Pr).astype(np.int64), cat(Pc).astype(np.int64))), shape=(ND, ND))
 
     def solve(self, b, exact=True):
         """M^-1 b by sparse LU (exact=False: SolverCG + PreconditionJacobi,
@@ -296,6 +308,126 @@ class CutAdvection2D:
                     e[off + 2] += float(np.sum(err * err * w))
         e[2], e[5] = math.sqrt(e[2]), math.sqrt(e[5])
         return tuple(e)
+
+
+class CutAdvectionField(CutAdvection2D):
+    """One field of the composite application (advection-app.cc:99-152;
+    problem.h:103-181): the same assembly on [lo, hi]^2 for the given vertex
+    level set and advection.  The outside field (location outside) is this
+    assembly on the negated level set: its inside is the outside region, the
+    face parts and MeshClassifier follow the sign, the Saye surface points of
+    a bilinear level set are the same and its normal is the flipped one of
+    stiffness.h:437, the ghost-penalty faces those of the inverse location
+    (stiffness.h:260-280, mass.h:67-104).  composite: (II)'s inflow is P
+    u_partner."""
+
+    def __init__(self, p, n_sub, lo, hi, ls_vertex, a, composite=True, gamma_M=0.5, gamma_A=0.5):
+        self.p, self.n = p, n_sub
+        self.gM, self.gA = gamma_M, gamma_A
+        self.a = np.asarray(a, dtype=np.float64)
+        self.composite = composite
+        self.geo = g = cut2d.CutPoisson2D(p, n_sub, lo, hi)
+        self.h, self.N = g.h, g.N
+        g.ls = np.asarray(ls_vertex, dtype=np.float64).reshape(self.N, self.N)
+        for cy in range(n_sub):
+            for cx in range(n_sub):
+                v = g.ls[cy:cy + 2, cx:cx + 2]
+                g.loc[cy, cx] = (cut2d.INSIDE if np.all(v < 0) else
+                                 (cut2d.OUTSIDE if np.all(v > 0) else cut2d.INTERSECTED))
+        self._assemble()
+
+    def exact(self, x, y, t):
+        return app_exact(x, y, t)
+
+
+def app_exact(x, y, t=0.0):
+    """advection-app.cc:50-64: max(0, 0.3 - |p - (-0.3, -0.3)|), time independent"""
+    return np.maximum(0.0, 0.3 - np.hypot(np.asarray(x) + 0.3, np.asarray(y) + 0.3))
+
+
+def app_exact_dt(x, y, t=0.0):
+    """advection-app.cc:66-81: 0"""
+    return np.zeros_like(np.asarray(x, dtype=np.float64))
+
+
+class CompositeAdvection2D:
+    """AdvectionProblem::run, composite branch (problem.h:103-181) with
+    advection-app.cc's preset (factor 27: phi = 135 deg, x_shift 0.25, level
+    set SignedDistance::Plane((x_shift, 0), (sin phi, -cos phi)), a = (3, 1)
+    inside, (1, 2) outside, p = 5, [-1, 1]^2, gamma_M = gamma_A = 0.5, cfl 0.2,
+    max_val 4, end_t 0.6; n_sub = 200 in the preset, any n here).  Block vector
+    (bc_in, u_in, bc_out, u_out), f = (dg/dt, M_in^-1 (K_in u_in + F_in bc_in +
+    P_in u_out), dg/dt, M_out^-1 (...)), RK_CLASSIC_FOURTH_ORDER over the whole
+    block vector, DiscreteTime, the loop's error[2] < 1 guard.  The mass solves
+    are the reference's SolverDirect branch (sparse LU).  The reference prints
+    nothing for this preset: parity unpinned beyond the non-composite pins
+    of the shared assembly (test_01.output)."""
+
+    def __init__(self, p=5, n_sub=200, end_t=0.6, cfl=0.2, factor=27.0, x_shift=0.25, a_in=(3.0, 1.0),
+                 a_out=(1.0, 2.0), lo=-1.0, hi=1.0, gamma_M=0.5, gamma_A=0.5, max_val=4.0):
+        phi = (math.pi * 5.0 / 180.0) * factor
+        nrm = (math.sin(phi), -math.cos(phi))
+        h = (hi - lo) / n_sub
+        xv = lo + np.arange(n_sub + 1) * h
+        xx, yy = np.meshgrid(xv, xv, indexing="xy")
+        self.ls = ((xx - x_shift) * nrm[0] + yy * nrm[1]).reshape(-1)
+        self.fields = [CutAdvectionField(p, n_sub, lo, hi, self.ls, a_in, True, gamma_M, gamma_A),
+                       CutAdvectionField(p, n_sub, lo, hi, -self.ls, a_out, True, gamma_M, gamma_A)]
+        self.dt = h * cfl / max_val
+        self.end_t, self.xv = end_t, xv
+
+    def rhs(self, t, y):
+        """the field blocks of fu_rhs before the mass solves: [rhs_in, rhs_out]"""
+        nb = [len(f.points) for f in self.fields]
+        bc_in, u_in = y[:nb[0]], y[nb[0]:nb[0] + self.n]
+        o = nb[0] + self.n
+        bc_out, u_out = y[o:o + nb[1]], y[o + nb[1]:]
+        fi, fo = self.fields
+        return (fi.K @ u_in + fi.F @ bc_in + fi.P @ u_out, fo.K @ u_out + fo.F @ bc_out + fo.P @ u_in)
+
+    @property
+    def n(self):
+        return self.fields[0].N ** 2
+
+    def run(self, max_steps=None):
+        fi, fo = self.fields
+        pin, pout = fi.points, fo.points
+        nb = [len(pin), len(pout)]
+        X, Y = np.meshgrid(self.xv, self.xv, indexing="xy")
+        u0 = app_exact(X.reshape(-1), Y.reshape(-1))
+        u_in, u_out = u0.copy(), u0.copy()
+        time = cut1d.DiscreteTime(0.0, self.end_t, self.dt)
+
+        def bcs(t):
+            return (app_exact(pin[:, 0], pin[:, 1], t) if nb[0] else np.zeros(0),
+                    app_exact(pout[:, 0], pout[:, 1], t) if nb[1] else np.zeros(0))
+
+        def f(t, y):
+            r_in, r_out = self.rhs(t, y)
+            d_in = app_exact_dt(pin[:, 0], pin[:, 1], t) if nb[0] else np.zeros(0)
+            d_out = app_exact_dt(pout[:, 0], pout[:, 1], t) if nb[1] else np.zeros(0)
+            return np.concatenate([d_in, fi.solve(r_in), d_out, fo.solve(r_out)])
+
+        rows = [(0, 0.0) + self.errors(u_in, u_out, 0.0)]
+        steps = 0
+        # the loop guard error[2] < 1: L2 of the outside field's postprocess, row entry 2 + 6 + 2
+        while not time.is_at_end() and rows[-1][10] < 1.0 and (max_steps is None or steps < max_steps):
+            b_in, b_out = bcs(time.t)  # initialize_time_step
+            y = np.concatenate([b_in, u_in, b_out, u_out])
+            y = cut1d.rk4_step(f, time.t, time.next_step_size(), y)
+            u_in = y[nb[0]:nb[0] + self.n]
+            u_out = y[nb[0] + self.n + nb[1]:]
+            t_end = time.t + time.next_step_size()
+            time.advance()
+            steps += 1
+            rows.append((steps, t_end) + self.errors(u_in, u_out, t_end))
+        self.u_in, self.u_out, self.steps = u_in, u_out, steps
+        return rows
+
+    def errors(self, u_in, u_out, t):
+        """postprocess(inside) then postprocess(outside) (problem.h:150-175): the six norms (Linf, L1, L2,
+        Linf_face, L1_face, L2_face) of each field"""
+        return tuple(self.fields[0].errors(u_in, t)) + tuple(self.fields[1].errors(u_out, t))
 
 
 def table_row(p, factor, n_sub=40):

@@ -44,8 +44,9 @@ def _lib():
 
     L = gdm_amd.load()
     P, I64, U32, D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32, ctypes.c_double
-    L.gdmh_cut_adv_create.argtypes = [ctypes.c_int, ctypes.c_int, D, D, P, P, D, D, ctypes.POINTER(P),
+    L.gdmh_cut_adv_create.argtypes = [ctypes.c_int, ctypes.c_int, D, D, P, P, D, D, ctypes.c_int, ctypes.POINTER(P),
                                       ctypes.c_char_p, ctypes.c_size_t]
+    L.gdmh_cut_adv_coupling.argtypes = [P] + [ctypes.POINTER(ctypes.c_void_p)] * 3 + [ctypes.POINTER(I64)]
     L.gdmh_cut_adv_info.argtypes = [P, ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(I64),
                                     ctypes.POINTER(I64)]
     L.gdmh_cut_adv_arrays.argtypes = [P] + [ctypes.POINTER(ctypes.c_void_p)] * 8
@@ -59,15 +60,16 @@ def _arr(ptr, n, dt):
     return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(dt)), shape=(n,)).copy() if n else np.zeros(0)
 
 
-def host_system(P):
-    """(C, F, M, zero_rows, bc points) as gdm_cut_advection_create assembles them"""
+def host_system(P, lo=0.0, hi=1.0, composite=False, coupling=None):
+    """(C, F, M, zero_rows, bc points) as gdm_cut_advection_create assembles them
+    (composite: also the partner coupling, appended to `coupling`)"""
     L = _lib()
     ls = np.ascontiguousarray(P.geo.ls.reshape(-1), dtype=np.float64)
     a = np.array(P.a, dtype=np.float64)
     S = ctypes.c_void_p()
     err = ctypes.create_string_buffer(256)
-    rc = L.gdmh_cut_adv_create(P.p, P.n, 0.0, 1.0, ls.ctypes.data, a.ctypes.data, P.gA, P.gM, ctypes.byref(S), err,
-                               256)
+    rc = L.gdmh_cut_adv_create(P.p, P.n, lo, hi, ls.ctypes.data, a.ctypes.data, P.gA, P.gM, int(composite),
+                               ctypes.byref(S), err, 256)
     assert rc == 0, err.value
     try:
         nd, nb, bw = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
@@ -91,14 +93,21 @@ def host_system(P):
         mrp = _arr(m[0], N + 1, ctypes.c_int64)
         M = sps.csr_matrix((_arr(m[2], mrp[-1], ctypes.c_double), _arr(m[1], mrp[-1], ctypes.c_uint32), mrp),
                            shape=(N, N))
+        if coupling is not None:
+            q = [ctypes.c_void_p() for _ in range(3)]
+            nnz = ctypes.c_int64()
+            L.gdmh_cut_adv_coupling(S, *[ctypes.byref(x) for x in q], ctypes.byref(nnz))
+            prp = _arr(q[0], N + 1, ctypes.c_int64) if composite else np.zeros(N + 1, dtype=np.int64)
+            coupling.append(sps.csr_matrix((_arr(q[2], nnz.value, ctypes.c_double),
+                                            _arr(q[1], nnz.value, ctypes.c_uint32), prp), shape=(N, N)))
     finally:
         L.gdmh_cut_adv_destroy(S)
     return C, F, M, zero, xy
 
 
-def box_operator(P):
+def box_operator(P, lo=0.0, hi=1.0):
     """the uncut fused stencil S of the box (2D advection with outflow traces), Kronecker form"""
-    m = O.Mesh(2, P.p, P.n, 0.0, 1.0)
+    m = O.Mesh(2, P.p, P.n, lo, hi)
     p = P.p
 
     def band(B):
@@ -153,3 +162,25 @@ def test_device_formulation_reproduces_test_01(row):
     for c, (g, w) in enumerate(zip((l2, l1, linf, l2_f, l1_f, linf_f), ref[5:])):
         e = math.floor(math.log10(abs(w)))
         assert abs(g - w) <= 0.5 * 10.0 ** (e - 4) * (1 + 1e-9) + slack, (GOLD["columns"][5 + c], g, w)
+
+
+def test_composite_host_matrices_match_oracle():
+    """advection-app.cc's composite preset at reduced n (30 cells on [-1, 1]^2,
+    p = 5): both fields' device matrices (the outside one assembled on the
+    negated level set) equal the oracle's -- K = Z S + C, F (box-face inflow
+    only: the surface points are no stage points), M, and the partner
+    coupling P of the cut-surface inflow (stiffness.h:448-453).  Parity of
+    the composite branch itself is unpinned (the reference prints nothing for
+    this preset)."""
+    c = CA.CompositeAdvection2D(n_sub=30, end_t=0.0)
+    for fld in c.fields:
+        cpl = []
+        C, F, M, zero, xy = host_system(fld, -1.0, 1.0, composite=True, coupling=cpl)
+        N = fld.N * fld.N
+        np.testing.assert_allclose(xy, fld.points, rtol=0, atol=1e-14)
+        K_dev = (_zero_proj(N, zero) @ box_operator(fld, -1.0, 1.0) + C).tocsr()
+        for A, B in ((K_dev, fld.K), (F, fld.F), (M, fld.M), (cpl[0], fld.P)):
+            D = (A - B).tocoo()
+            assert (abs(D.data).max() if D.nnz else 0.0) <= 1e-13 * max(abs(B).max(), 1e-300)
+    # the flow crosses the plane from the inside field into the outside one
+    assert c.fields[0].P.nnz == 0 and c.fields[1].P.nnz > 0

@@ -95,3 +95,57 @@ def test_device_run_reproduces_test_01_row(row):
         # test_cut_advection_host.py)
         slack = 5e-13 if p == 3 else 3e-12
         assert abs(g - w) <= 0.5 * 10.0 ** (e - 4) * (1 + 1e-9) + slack, (GOLD["columns"][5 + c], g, w)
+
+
+def _composite_device(c, n_sub):
+    import gdm_amd
+
+    return gdm_amd.CutAdvectionCompositeProblem(5, n_sub, -1.0, 1.0, c.ls, (3.0, 1.0), (1.0, 2.0), CA.app_exact,
+                                                CA.app_exact_dt)
+
+
+def test_composite_compute_rhs_matches_oracle():
+    """advection-app.cc's composite preset (reduced n): each field's
+    compute_rhs + partner coupling on random (bc_in, u_in, bc_out, u_out)
+    against the oracle's K u + F bc + P u_partner (stiffness.h:196-214,
+    448-453).  Parity unpinned: the reference prints nothing for the preset;
+    the oracle's shared assembly is pinned by test_01."""
+    n_sub = 30
+    c = CA.CompositeAdvection2D(n_sub=n_sub, end_t=0.0)
+    prob = _composite_device(c, n_sub)
+    rng = np.random.default_rng(31)
+    fi, fo = c.fields
+    nb = [len(fi.points), len(fo.points)]
+    assert [ca.n_bc_points for ca in prob.f] == nb
+    for ca, fld in zip(prob.f, c.fields):
+        np.testing.assert_allclose(ca.bc_points(), fld.points, rtol=0, atol=1e-14)
+    y = [rng.uniform(-1, 1, n) for n in (nb[0], c.n, nb[1], c.n)]
+    ref_in, ref_out = c.rhs(0.0, np.concatenate(y))
+    for i, (ca, ref) in enumerate(zip(prob.f, (ref_in, ref_out))):
+        out = ca.new_vector()
+        ca.compute_rhs(torch.from_numpy(y[2 * i + 1]).cuda(), torch.from_numpy(y[2 * i]).cuda(), out)
+        ca.couple(torch.from_numpy(y[3 - 2 * i]).cuda(), out)
+        got = out.cpu().numpy()
+        assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 1e-12
+
+
+def test_composite_run_matches_oracle():
+    """AdvectionProblem::run's composite branch (problem.h:103-181): 12 RK4
+    steps of the preset at n = 30 on the device vs the oracle (both fields'
+    final DoF vectors over their regions and the printed postprocess norms).
+    Parity unpinned (see above)."""
+    n_sub, steps = 30, 12
+    c = CA.CompositeAdvection2D(n_sub=n_sub)
+    rows = c.run(max_steps=steps)
+    prob = _composite_device(c, n_sub)
+    assert prob.run(0.0, c.end_t, c.dt, max_steps=steps) == steps == c.steps
+    u_in, u_out = prob.y[1].cpu().numpy(), prob.y[3].cpu().numpy()
+    for fld, u, uref in ((c.fields[0], u_in, c.u_in), (c.fields[1], u_out, c.u_out)):
+        ex = fld.exact
+        fld.exact = lambda x, y, t: np.zeros_like(np.asarray(x, dtype=np.float64))
+        d_l2 = fld.errors(u - uref, 0.0)[2]
+        r_l2 = fld.errors(uref, 0.0)[2]
+        fld.exact = ex
+        assert d_l2 <= 1e-9 * r_l2, (d_l2, r_l2)
+    got = c.errors(u_in, u_out, rows[-1][1])
+    np.testing.assert_allclose(got, rows[-1][2:], rtol=1e-8, atol=1e-14)

@@ -59,6 +59,24 @@ def test_mpi_driver_matches_single_rank(tmp_path, dim, p, n, steps, np_):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not HAVE_MPI, reason="MPI runtime or the MPI host programs missing")
+@pytest.mark.parametrize("dim,p,n,np_", [(3, 5, 30, 2), (3, 3, 20, 3), (3, 5, 14, 2)])
+def test_overlapped_exchange_bitwise_equals_blocking(tmp_path, dim, p, n, np_):
+    """compute_rhs_overlapped (interior planes while MpiRank's messages are in
+    flight, the slab-edge planes after them) gives the same bits as
+    update_ghost_values + compute_rhs (advection/stiffness.h:343, 345-605)."""
+    outs = []
+    for kind in ("mpi", "mpi-blocking"):
+        out = tmp_path / ("u_%s.bin" % kind)
+        r = _mpirun(np_, [os.path.join(HOST, "advection_app_mpi"), str(dim), str(p), str(n), "2", "0.1", str(out),
+                          "1", kind], timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert ("exchange blocking" in r.stdout) == kind.endswith("blocking")
+        outs.append(np.fromfile(out, dtype=np.float64))
+    assert outs[0].size > 0 and np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not HAVE_MPI, reason="MPI runtime or the MPI host programs missing")
 def test_rccl_communicator_one_rank(tmp_path):
     out1, outr = tmp_path / "u1.bin", tmp_path / "ur.bin"
     args = ["3", "5", "14", "2", "0.1"]
