@@ -74,6 +74,7 @@ struct Face {
   FaceDir t0, t1;
   int64_t base = 0;       // owned index of node (i0 = 0, i1 = t1.node_begin)
   double *T = nullptr;    // step-1 scratch of this face (faces run concurrently)
+  double *G = nullptr;    // step-2 result of this face (node-major [i1][i0]), added after the join
 };
 
 }  // namespace
@@ -644,6 +645,10 @@ void build_faces(gdm_op *op) {
       const int64_t tsz = std::max<int64_t>(1, (int64_t)F.t1.Q * (F.t0.node_end - F.t0.node_begin));
       hip_check(hipMalloc(&F.T, sizeof(double) * tsz), "hipMalloc");
       keep(op, F.T);
+      const int64_t gsz = std::max<int64_t>(1, (int64_t)(F.t0.node_end - F.t0.node_begin) *
+                                                   (F.t1.node_end - F.t1.node_begin));
+      hip_check(hipMalloc(&F.G, sizeof(double) * gsz), "hipMalloc");
+      keep(op, F.G);
     }
     op->faces.push_back(F);
   }
@@ -752,7 +757,12 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
   // table kernel, both ranges of it in one launch.
   const int p = op->p, zlo = 3 * p + 1, zhi = a.Nz - 3 * p - 1;
   const int i0 = std::max(zb, zlo), i1 = std::min(ze, zhi);
-  const bool split = a.z_toep && i1 - i0 >= 2 * p + 1;
+  // every plane in [zlo, zhi) goes to the compile-time-band kernel, whatever
+  // the launched range: the table rows of the interior column round
+  // differently, so a plane range (gdm_apply_planes, the overlapped exchange)
+  // must pick the same kernel per plane as the whole launch to give the same
+  // bits (tests/test_host_mpi.py)
+  const bool split = a.z_toep && i1 > i0;
   const int ty = ty8, wgs = wgs8;
   const int64_t tiles = (int64_t)((a.Nx + 63) / 64) * ((a.out_y1 - a.out_y0 + ty - 1) / ty);
   // one round of workgroups on 256 CUs (two rounds measured 0.93 vs 0.85 ms
@@ -783,7 +793,8 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
 }
 
 // phase 0: both steps on op->stream; 1: step 1 (bc values -> per-face T) on
-// stream `st`; 2: step 2 (T -> dst) on op->stream
+// stream `st`; 2: step 2 (T -> dst) on op->stream; 3: both steps into the
+// per-face buffers G on stream `st`; 4: dst += G on op->stream
 void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
                           hipStream_t st = nullptr) {
   if (op->kind != GDM_OP_ADVECTION) return;
@@ -812,6 +823,7 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     fa.ncell0_total = F.t0.ncell_total;
     fa.cell0_begin = F.t0.cell_begin;
     fa.T = F.T ? F.T : op->face_tmp;
+    fa.G = F.G;
     fa.dst = dst_owned;
     fa.base = F.base;
     fa.stride0 = F.t0.stride;
@@ -821,8 +833,12 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     // one face after the other: two faces share the box-edge nodes, and a
     // concurrent step 2 (one launch, fp64 atomics on the edges) made the
     // edge sums order-dependent, which the bit-exact rank / communicator
-    // comparisons of tests/test_host_mpi.py catch
-    hip_check(gdmk_launch_face(fa, phase == 1 && st ? st : op->stream), "face launch");
+    // comparisons of tests/test_host_mpi.py catch.  Phase 3 (side stream)
+    // computes every face's step 2 into its own buffer G while the stencil
+    // runs; phase 4 adds the buffers into dst face by face in the same order
+    // (the same roundings as phase 0's dst += scale s)
+    if (phase == 3 && !F.G) fa.phase = 1;  // (no buffer: cannot happen for inflow faces)
+    hip_check(gdmk_launch_face(fa, (phase == 1 || phase == 3) && st ? st : op->stream), "face launch");
   }
 }
 
@@ -1037,6 +1053,9 @@ void build_spike(gdm_op *op) {
 
 // the line solves of M^-1 along every kernel axis; `part` replaces the
 // partitioned axis' tables by the slab's diagonal block (multi-rank)
+#ifndef GDM_MASS_X_STRIDED
+#define GDM_MASS_X_STRIDED 0
+#endif
 void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, const LineTables *part) {
   const int64_t n = op->layout.n_owned;
   if (n <= 0) return;
@@ -1073,7 +1092,13 @@ void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
   const bool part_z = part && op->part_axis == 2, part_y = part && op->part_axis == 1;
   if (Z > 1 || part_z) passes.push_back({2, 1, Z, X * Y, X * Y, X * Y, 0, "mass z"});  // base = l, step X*Y
   if (Y > 1 || part_y) passes.push_back({1, 1, Y, X, X * Z, X, X * Y, "mass y"});      // base = z*X*Y + x, step X
+#if GDM_MASS_X_STRIDED
+  // x lines through the strided (lane = line) kernel: line l at l X, step 1 -- every load / store instruction
+  // touches 64 rows; no LDS staging, so four waves per CU
+  if (X > 1) passes.push_back({0, 1, X, 1, Y * Z, 1, X, "mass x"});
+#else
   if (X > 1) passes.push_back({0, 0, X, 1, Y * Z, 1, 0, "mass x"});                   // contiguous rows of length X
+#endif
   auto use_v3 = [&](const Pass &q, const double *src, const double *dst) {
     const LineTables &t = tab[q.ax];
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
@@ -1082,7 +1107,8 @@ void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
     // line span (len - 1) * stride plus the 64 lanes must stay below 2^31
     // bytes (3D meshes up to 645 vertices per direction), else the v2 kernel
     // (64-bit addresses) runs
-    const bool span_ok = q.dir_kind != 1 || ((q.len - 1) * q.stride + 64) * 8 < (int64_t)0x7fffffff;
+    const int64_t lanes = q.A == 1 ? 63 * q.B + 1 : 64;  // a wave's lane span (A = 1: x lines, B apart)
+    const bool span_ok = q.dir_kind != 1 || ((q.len - 1) * q.stride + lanes) * 8 < (int64_t)0x7fffffff;
     return v3 && t.l3 && span_ok && (q.dir_kind == 1 || (q.len % 2 == 0 && aligned));
   };
   bool segmented = false;
@@ -1387,10 +1413,10 @@ int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const doub
     hip_check(hipStreamWaitEvent(op->side_stream, op->ev_fork, 0), "hipStreamWaitEvent");
     hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, -1, -1, op->side_stream),
               "stencil launch");
-    if (bc_values) launch_boundary_data(op, bc_values, dst_owned, 1, op->side_stream);
+    if (bc_values) launch_boundary_data(op, bc_values, dst_owned, 3, op->side_stream);
     hip_check(hipEventRecord(op->ev_join, op->side_stream), "hipEventRecord");
     hip_check(hipStreamWaitEvent(op->stream, op->ev_join, 0), "hipStreamWaitEvent");
-    if (bc_values) launch_boundary_data(op, bc_values, dst_owned, 2);
+    if (bc_values) launch_boundary_data(op, bc_values, dst_owned, 4);
   } else {
     any_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned);
     if (bc_values) launch_boundary_data(op, bc_values, dst_owned);
@@ -2184,9 +2210,16 @@ int gdm_cut_advection_create2(int fe_degree, int n_subdivisions, double left, do
       const double *pv;
       int64_t pnnz = 0;
       gdmh_cut_adv_coupling(c->host, &prp, &pci, &pv, &pnnz);
+      // (a field the flow only leaves through the surface has no coupling entries: pci / pv may be NULL)
+      std::vector<uint32_t> ci(std::max<int64_t>(pnnz, 1), 0u);
+      std::vector<double> cv(std::max<int64_t>(pnnz, 1), 0.0);
+      if (pnnz > 0) {
+        std::copy(pci, pci + pnnz, ci.begin());
+        std::copy(pv, pv + pnnz, cv.begin());
+      }
       c->p_rp = dev_upload(std::vector<int64_t>(prp, prp + N + 1));
-      c->p_ci = dev_upload(std::vector<uint32_t>(pci, pci + std::max<int64_t>(pnnz, 1)));
-      c->p_v = dev_upload(std::vector<double>(pv, pv + std::max<int64_t>(pnnz, 1)));
+      c->p_ci = dev_upload(ci);
+      c->p_v = dev_upload(cv);
     }
   } catch (...) {
     c->release();

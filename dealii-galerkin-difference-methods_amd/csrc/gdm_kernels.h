@@ -75,10 +75,12 @@ struct FaceArgs {
   const int *crange0;
   int p, ncell0_total, cell0_begin;
   double *T;  // scratch Q1 x (i0_end - i0_begin)
+  double *G;  // phases 3 / 4: the step-2 result [i1][i0] of the face
   double *dst;
   int64_t base, stride0, stride1;  // dst offset of node (i0_begin, i1_begin)
   double scale;
-  int phase;  // 0: both steps, 1: step 1 only (writes T), 2: step 2 only (T -> dst)
+  int phase;  // 0: both steps, 1: step 1 only (writes T), 2: step 2 only (T -> dst),
+              // 3: both steps into G (G = scale s), 4: dst += G
 };
 
 constexpr int FACE_CHUNK = 256;  // t0 nodes per workgroup of the face row kernel

@@ -45,6 +45,11 @@
 // nt) and its output stores (1 = non-temporal).  A/B at C3 on the MI355X
 // (profiles/r3x, 3 repetitions each): cached 0.840-0.849 ms, non-temporal
 // stores 0.822-0.837 ms (the default), non-temporal stores and DMA 0.835-0.845
+// producers issue the next plane's DMA per row group right after reading the
+// group's window (before its FMAs) instead of after the whole x-sweep
+#ifndef GDM_EARLY_DMA
+#define GDM_EARLY_DMA 0
+#endif
 #ifndef GDM_STENCIL_LD_CPOL
 #define GDM_STENCIL_LD_CPOL 0
 #endif
@@ -290,6 +295,33 @@ __device__ __forceinline__ void stage_plane_pre7(const StencilArgs &a, const Til
           else
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, d.vo[ps][i], 0, 0, GDM_STENCIL_LD_CPOL);
         }
+      }
+    }
+  }
+}
+
+// the DMA of one pass (row group t.wv + ps NP) of plane zz
+template <int P, int R, int NC, int NP, int BK, int CH>
+__device__ __forceinline__ void stage_pass_pre7(const StencilArgs &a, const Tile7 &t, int zz, ldouble *ubuf,
+                                                const DmaPre7<P, R, NC, NP, BK, CH> &d, int ps) {
+  using G = Geom7<P, R, NC, NP, BK>;
+  using S = Dma7<P, R, NC, NP, BK, CH>;
+  const int ny_in = a.in_y1 - a.in_y0;
+  const double *plane = a.src + (int64_t)(zz - a.in_z0) * ny_in * a.Nx;
+  const int nbytes = (int)((int64_t)ny_in * a.Nx * 8);
+  __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)plane, 0, nbytes, 0x00020000);
+  const int g = t.wv + ps * NP;
+  if (g < G::NG) {
+    const int ni = g == G::NG - 1 ? S::NI_LAST : S::NI_FULL;
+    auto *gbase = (__attribute__((address_space(3))) char *)(ubuf + g * 4 * G::RL);
+#pragma unroll
+    for (int i = 0; i < S::NI_FULL; ++i) {
+      if (i < ni && d.vo[ps][i] != 0xffffffffu) {
+        auto *dst = (__attribute__((address_space(3))) void *)(gbase + i * 64 * CH);
+        if constexpr (CH == 16)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, d.vo[ps][i], 0, 0, GDM_STENCIL_LD_CPOL);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, d.vo[ps][i], 0, 0, GDM_STENCIL_LD_CPOL);
       }
     }
   }
@@ -711,24 +743,33 @@ __device__ __forceinline__ void wait_dma_planes(int wv) {
 }
 
 // x-sweep of row group g (pass of this producer wave) into registers:
-// A = mhat*u (+ wall rows), B = sx bhat*u (+ wall rows), 4 consecutive x per lane
+// A = mhat*u (+ wall rows), B = sx bhat*u (+ wall rows), 4 consecutive x per lane.
+// xload8 reads the lane's 16-B aligned window of the group's plane rows from
+// LDS, xcalc8 computes from it (split so that a producer can release the u
+// slot -- and issue the next DMA into it -- before the FMAs).
 template <int P, int R, int NC, int NP, int BK>
-__device__ __forceinline__ void xsweep8(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g, dpair (&V)[4]) {
-  // V[j] = (A_j, B_j) for x = 4 q + j (the pair the AB plane stores, so no
-  // register moves before the b128 stores); mass: V[0] = (A_0, A_1), V[1] = (A_2, A_3)
+__device__ __forceinline__ void xload8(const Tile7 &t, lcdouble *us, int g, double (&w)[Geom8<P, R, NC, NP, BK>::NWIN]) {
   using G = Geom8<P, R, NC, NP, BK>;
-  using IR = InteriorRows<P>;
-  constexpr int W = G::W, RL = G::RL;
+  constexpr int RL = G::RL;
   const int rr = t.lane >> 4, q = t.lane & 15;
   const int r = 4 * g + rr;
   lcdouble2 *wp = (lcdouble2 *)(us + r * RL + 4 * q);
-  double w[G::NWIN];
 #pragma unroll
   for (int i = 0; i < G::NWIN / 2; ++i) {
     const dpair v = wp[i];
     w[2 * i] = v.x;
     w[2 * i + 1] = v.y;
   }
+}
+
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void xcalc8(const StencilArgs &a, const double (&w)[Geom8<P, R, NC, NP, BK>::NWIN],
+                                       dpair (&V)[4]) {
+  // V[j] = (A_j, B_j) for x = 4 q + j (the pair the AB plane stores, so no
+  // register moves before the b128 stores); mass: V[0] = (A_0, A_1), V[1] = (A_2, A_3)
+  using G = Geom8<P, R, NC, NP, BK>;
+  using IR = InteriorRows<P>;
+  constexpr int W = G::W;
 #pragma unroll
   for (int j = 0; j < 4; ++j) V[j] = dpair{0.0, 0.0};
   if (a.x_toep) {
@@ -755,6 +796,13 @@ __device__ __forceinline__ void xsweep8(const StencilArgs &a, const Tile7 &t, lc
 #pragma unroll
     for (int j = 0; j < 4; ++j) V[j].y *= a.sx;
   }
+}
+
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void xsweep8(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g, dpair (&V)[4]) {
+  double w[Geom8<P, R, NC, NP, BK>::NWIN];
+  xload8<P, R, NC, NP, BK>(t, us, g, w);
+  xcalc8<P, R, NC, NP, BK>(a, w, V);
 }
 
 // Wall columns of row group g (first / last x tiles only): the
@@ -927,6 +975,29 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
       Tile7 tt = t;
       tt.ab0 = t.ab0 + slot * G::ABSZ;
       GDM_STAMPT(t, i, 1);
+#if GDM_EARLY_DMA
+      // per row group: read the group's window (and x-wall taps) from the u
+      // slot, then issue DMA(i + 2) of the group into the rows just read,
+      // then the FMAs -- the next plane's fetch starts one x-sweep earlier
+#pragma unroll
+      for (int ps = 0; ps < G::NPASS; ++ps) {
+        const int g = t.wv + ps * NP;
+        if (g < G::NG) {
+          double w[G::NWIN];
+          xload8<P, R, NC, NP, BK>(tt, u[slot], g, w);
+          XWall<P, BK> xw0;
+          if (t.ncw > 0) xwall8_calc<P, R, NC, NP, BK>(tt, u[slot], g, xpre, xw0);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (i + 2 < n && !GDM_DBG(a, 8)) stage_pass_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre, ps);
+          xcalc8<P, R, NC, NP, BK>(a, w, V1);
+          if (!GDM_DBG(a, 64)) write_ab8<P, R, NC, NP, BK>(tt, g, V1);
+          if (t.ncw > 0) xwall8_add<P, BK>(tt, xw0);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      GDM_STAMPT(t, i, 2);
+      GDM_STAMPT(t, i, 3);
+#else
 #pragma unroll
       for (int ps = 0; ps < G::NPASS; ++ps) {
         const int g = t.wv + ps * NP;
@@ -947,6 +1018,7 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
       GDM_STAMPT(t, i, 2);
       if (i + 2 < n && !GDM_DBG(a, 8)) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre);
       GDM_STAMPT(t, i, 3);
+#endif
       if (!GDM_DBG(a, 16)) GDM_LDS_BARRIER();  // B_i: AB(i) complete
       GDM_STAMPT(t, i, 4);
       if (t.yedge) {
@@ -1749,6 +1821,11 @@ __global__ void __launch_bounds__(512) face_cell_step1_kernel(const double *__re
   }
 }
 
+// dst node (t, i1) += scale sum_m w1[i1][m] T[q + m][t].  The product is
+// rounded before the add (no FMA contraction into it), so the result equals
+// G = scale s then dst + G (ASSIGN: G written node-major, added by
+// face_add_kernel after the stencil): the same bits on both paths.
+template <bool ASSIGN>
 __global__ void __launch_bounds__(256) face_step2_kernel(const double *__restrict__ T, int n0, int i1_begin,
                                                           int i1_end, const int *__restrict__ qs1,
                                                           const int *__restrict__ qc1,
@@ -1762,8 +1839,31 @@ __global__ void __launch_bounds__(256) face_step2_kernel(const double *__restric
   const int n = qc1[i1], q = qs1[i1];
   double s = 0.0;
   for (int m = 0; m < n; ++m) s = fma(w[m], T[(int64_t)(q + m) * n0 + t], s);
-  double *d = dst + base + (int64_t)t * stride0 + (int64_t)(i1 - i1_begin) * stride1;
-  *d += scale * s;
+  // the product is rounded on its own: the compiler may not fuse it into the
+  // add below (one FMA would round differently from G + dst)
+  double v;
+  {
+#pragma clang fp contract(off)
+    v = scale * s;
+  }
+  asm volatile("" : "+v"(v));
+  if constexpr (ASSIGN) {
+    dst[(int64_t)(i1 - i1_begin) * n0 + t] = v;
+  } else {
+    double *d = dst + base + (int64_t)t * stride0 + (int64_t)(i1 - i1_begin) * stride1;
+    *d = *d + v;
+  }
+}
+
+// dst node (t, i1) += G[i1][t]: one launch per face, in face order
+__global__ void __launch_bounds__(256) face_add_kernel(const double *__restrict__ G, int n0, int n1,
+                                                        double *__restrict__ dst, int64_t base, int64_t stride0,
+                                                        int64_t stride1) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n0 * n1) return;
+  const int i1 = (int)(e / n0), t = (int)(e - (int64_t)i1 * n0);
+  double *d = dst + base + (int64_t)t * stride0 + (int64_t)i1 * stride1;
+  *d = *d + G[e];
 }
 
 // ---------------------------------------------------------------------------
@@ -2026,6 +2126,21 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
   using namespace gdmk;
   const int n0 = f.i0_end - f.i0_begin;
   if (n0 <= 0 || f.Q1 <= 0 || f.i1_end <= f.i1_begin) return hipSuccess;
+  if (f.phase == 4) {
+    const int n1 = f.i1_end - f.i1_begin;
+    const int64_t ne = (int64_t)n0 * n1;
+    hipLaunchKernelGGL(face_add_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, f.G, n0, n1, f.dst,
+                       f.base, f.stride0, f.stride1);
+    return hipGetLastError();
+  }
+  auto step2 = [&](dim3 g2) {
+    if (f.phase == 3)
+      hipLaunchKernelGGL(face_step2_kernel<true>, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1,
+                         f.w1, f.wmax1, f.G, (int64_t)0, (int64_t)1, (int64_t)n0, f.scale);
+    else
+      hipLaunchKernelGGL(face_step2_kernel<false>, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1,
+                         f.w1, f.wmax1, f.dst, f.base, f.stride0, f.stride1, f.scale);
+  };
   const size_t cell_lds = sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)f.Q0);
   if (f.phi0 && cell_lds <= 48 * 1024) {
     // cell form of step 1, then the usual step 2
@@ -2042,9 +2157,7 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
       default: return hipErrorInvalidValue;
     }
     dim3 g2((n0 + 255) / 256, f.i1_end - f.i1_begin);
-    if (f.phase != 1)
-      hipLaunchKernelGGL(face_step2_kernel, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1,
-                         f.wmax1, f.dst, f.base, f.stride0, f.stride1, f.scale);
+    if (f.phase != 1) step2(g2);
     return hipGetLastError();
   }
   dim3 b(256);
@@ -2066,9 +2179,7 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
     hipLaunchKernelGGL(face_step1_kernel<1>, g1, dim3(FACE_CHUNK), lds, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
                        f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
   dim3 g2((n0 + 255) / 256, f.i1_end - f.i1_begin);
-  if (f.phase != 1)
-    hipLaunchKernelGGL(face_step2_kernel, g2, b, 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1,
-                       f.dst, f.base, f.stride0, f.stride1, f.scale);
+  if (f.phase != 1) step2(g2);
   return hipGetLastError();
 }
 

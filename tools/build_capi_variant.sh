@@ -1,0 +1,10 @@
+# like tools/build_variant.sh but for the mass solve (capi + mass objects)
+NAME=$1; shift
+C=/root/repo/dealii-galerkin-difference-methods_amd/csrc
+B=/root/repo/dealii-galerkin-difference-methods_amd/lib/obj
+O=/root/repo/dealii-galerkin-difference-methods_amd/lib/variants/$NAME
+mkdir -p $O
+F="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -Wno-unused-function $*"
+/opt/rocm/bin/hipcc $F -x hip -c $C/gdm_capi.cpp -o $O/capi.o &&
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libgdm_hip.so $O/capi.o $B/gdm_kernels.o $B/gdm_setup.o \
+  $B/gdm_csr.o $B/gdm_mass.o $B/gdm_rk.o $B/gdm_post.o $B/gdm_cut.o $B/gdm_cut_advection.o $B/gdm_cut_wave.o $B/gdm_band.o && echo "built $O"
