@@ -154,6 +154,8 @@ struct gdm_op {
   double *err_S = nullptr, *err_partial = nullptr;
   static constexpr int n_err_partial = 1024;
   int bc_tab_ld = 0;
+  double *bc_stage_tab = nullptr;  // gdm_apply_bc_fn: BcStage factor tables (2 x 6 faces)
+  int bc_stage_ld = 0;
   // periodicity constraints (system.h:427-463): scratch copy of the input for
   // distribute; CG work vectors and the Jacobi inverse diagonal
   double *pscratch = nullptr;
@@ -795,13 +797,23 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
 // phase 0: both steps on op->stream; 1: step 1 (bc values -> per-face T) on
 // stream `st`; 2: step 2 (T -> dst) on op->stream; 3: both steps into the
 // per-face buffers G on stream `st`; 4: dst += G on op->stream
+// stage (non-NULL): the boundary values are evaluated from its function
+// (gdm_apply_bc_fn) instead of read from bc_values
 void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
-                          hipStream_t st = nullptr) {
+                          hipStream_t st = nullptr, const gdmk::BcStage *stage = nullptr) {
   if (op->kind != GDM_OP_ADVECTION) return;
-  for (const Face &F : op->faces) {
+  for (size_t fi = 0; fi < op->faces.size(); ++fi) {
+    const Face &F = op->faces[fi];
     if (F.scale == 0.0) continue;
     gdmk::FaceArgs fa{};
-    fa.U = bc_values + F.offset;
+    gdmk::BcStage fs{};
+    if (stage) {
+      fs = *stage;
+      fs.face = (int)fi;
+      fa.stage = &fs;
+    } else {
+      fa.U = bc_values + F.offset;
+    }
     fa.Q0 = F.t0.Q;
     fa.Q1 = F.t1.Q;
     fa.i0_begin = F.t0.node_begin;
@@ -1698,17 +1710,24 @@ int gdm_vec_rk_update(gdm_op *op, int64_t n, double beta, const double *k, const
   GDM_GUARD_END
 }
 
-int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_params, double t, int derivative,
-                      double *bc_values) {
-  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
-  if (op->layout.n_bc_points > 0 && !bc_values) return fail(GDM_ERR_ARG, "NULL bc_values");
+}  // extern "C"
+
+namespace {
+
+// argument checks of the built-in boundary functions (gdm_fn_kind); 0 = ok
+int check_bc_fn(gdm_op *op, int fn_kind, const double *params, int n_params) {
   const int need[3] = {1, 1 + op->dim, 9};
   if (fn_kind < 0 || fn_kind > 2) return fail(GDM_ERR_ARG, "unknown gdm_fn_kind");
   if (n_params < need[fn_kind] || (n_params > 0 && !params)) return fail(GDM_ERR_ARG, "too few function parameters");
-  if (op->faces.size() > 6 || op->p + 1 > 10) return fail(GDM_ERR_UNSUPPORTED, "boundary geometry");
-  GDM_GUARD_BEGIN
-  hip_check(hipSetDevice(op->device), "hipSetDevice");
-  gdmk::BcGeom g{};
+  if (op->faces.size() > (size_t)gdmk::BcStage::kMaxFaces || op->p + 1 > 10)
+    return fail(GDM_ERR_UNSUPPORTED, "boundary geometry");
+  return GDM_OK;
+}
+
+// the boundary-point geometry (device block(0) order) and the function
+void build_bc_fn(gdm_op *op, int fn_kind, const double *params, int n_params, gdmk::BcGeom &g, gdmk::BcFn &fn,
+                 int &ld) {
+  g = gdmk::BcGeom{};
   g.dim = op->dim;
   g.p = op->p;
   g.n_faces = (int)op->faces.size();
@@ -1732,12 +1751,29 @@ int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_param
       B.cell_begin[k] = T[k]->cell_begin;
     }
   }
-  gdmk::BcFn fn{};
+  fn = gdmk::BcFn{};
   fn.kind = fn_kind;
   fn.dim = op->dim;
   for (int i = 0; i < n_params && i < 12; ++i) fn.prm[i] = params[i];
-  int ld = 1;
+  ld = 1;
   for (const Face &F : op->faces) ld = std::max({ld, F.t0.Q, F.t1.Q});
+}
+
+}  // namespace
+
+extern "C" {
+
+int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_params, double t, int derivative,
+                      double *bc_values) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_bc_points > 0 && !bc_values) return fail(GDM_ERR_ARG, "NULL bc_values");
+  if (int rc = check_bc_fn(op, fn_kind, params, n_params)) return rc;
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  gdmk::BcGeom g;
+  gdmk::BcFn fn;
+  int ld = 1;
+  build_bc_fn(op, fn_kind, params, n_params, g, fn, ld);
   if (!op->bc_tab || op->bc_tab_ld < ld) {
     std::vector<double> zero((size_t)6 * 3 * ld * 2, 0.0);
     op->bc_tab = keep(op, dev_upload(zero));
@@ -1745,6 +1781,51 @@ int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_param
   }
   hip_check(gdmk_launch_bc_eval(g, fn, t, derivative ? 1 : 0, bc_values, op->bc_tab, op->bc_tab_ld, op->stream),
             "bc_eval");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_apply_bc_fn(gdm_op *op, const double *src_local, double *dst_owned, int fn_kind, const double *params,
+                    int n_params, double t_g, double alpha, double t_k) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
+  if (op->kind != GDM_OP_ADVECTION) return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_bc_fn: advection operators only");
+  if (int rc = check_bc_fn(op, fn_kind, params, n_params)) return rc;
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  gdmk::BcStage stage{};
+  int ld = 1;
+  build_bc_fn(op, fn_kind, params, n_params, stage.g, stage.f, ld);
+  if (!op->bc_stage_tab || op->bc_stage_ld < ld) {
+    std::vector<double> zero((size_t)2 * gdmk::BcStage::kMaxFaces * 3 * ld * 2, 0.0);
+    op->bc_stage_tab = keep(op, dev_upload(zero));
+    op->bc_stage_ld = ld;
+  }
+  stage.tab = op->bc_stage_tab;
+  stage.ld = op->bc_stage_ld;
+  stage.alpha = alpha;
+  const bool bc = op->layout.n_bc_points > 0;
+  const int with_k = alpha != 0.0 ? 1 : 0;
+  if (op->concurrent && !op->mesh.periodic) {
+    // as gdm_apply: the factor tables, the z-wall launch and the faces' step 1
+    // + 2 (into G) on the side stream, dst += G after the join
+    hip_check(hipEventRecord(op->ev_fork, op->stream), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(op->side_stream, op->ev_fork, 0), "hipStreamWaitEvent");
+    if (bc)
+      hip_check(gdmk_launch_bc_tables(stage.g, stage.f, t_g, t_k, with_k, op->bc_stage_tab, stage.ld, op->side_stream),
+                "bc tables");
+    hip_check(launch_stencil(op, false, src_local, dst_owned, -1, -1, op->side_stream), "stencil launch");
+    if (bc) launch_boundary_data(op, nullptr, dst_owned, 3, op->side_stream, &stage);
+    hip_check(hipEventRecord(op->ev_join, op->side_stream), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(op->stream, op->ev_join, 0), "hipStreamWaitEvent");
+    if (bc) launch_boundary_data(op, nullptr, dst_owned, 4);
+  } else {
+    if (bc)
+      hip_check(gdmk_launch_bc_tables(stage.g, stage.f, t_g, t_k, with_k, op->bc_stage_tab, stage.ld, op->stream),
+                "bc tables");
+    any_stencil(op, false, src_local, dst_owned);
+    if (bc) launch_boundary_data(op, nullptr, dst_owned, 0, nullptr, &stage);
+  }
   return GDM_OK;
   GDM_GUARD_END
 }

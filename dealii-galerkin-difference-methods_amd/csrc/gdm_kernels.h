@@ -5,6 +5,8 @@
 
 #include <atomic>
 
+#include "gdm_rk.h"
+
 namespace gdmk {
 
 // Fused Kronecker stencil: out = B_x M_y M_z + M_x B_y M_z + M_x M_y B_z (or
@@ -61,6 +63,7 @@ struct StencilArgs {
 // t0, t1; trivial directions have one node, one point and weight 1).
 struct FaceArgs {
   const double *U;  // [Q1][Q0] stage boundary values of the face
+  const BcStage *stage;  // or (non-NULL) evaluated from a built-in function (gdm_apply_bc_fn)
   int Q0, Q1;
   int i0_begin, i0_end, i1_begin, i1_end;  // owned output nodes
   const int *qs0, *qs1, *qc1;

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "gdm_bcfn.h"
 #include "gdm_coeffs.h"
 #include "gdm_kernels.h"
 
@@ -1730,8 +1731,20 @@ __global__ void __launch_bounds__(256) chol_lines_kernel(double *__restrict__ v,
 // in LDS with coalesced loads; each lane then owns one node and reads its
 // weights node-minor (w0T), so every global access is a contiguous wave row.
 // ---------------------------------------------------------------------------
-template <int ROWS>
-__global__ void __launch_bounds__(FACE_CHUNK) face_step1_kernel(const double *__restrict__ U, int Q0, int Q1,
+// boundary values U(i0, i1) of the face: stored ([Q1][Q0] array, gdm_apply)
+// or evaluated from a built-in function at the stage time (gdm_apply_bc_fn)
+struct BcArr {
+  const double *__restrict__ U;
+  int Q0;
+  __device__ __forceinline__ double operator()(int i0, int i1) const { return U[(int64_t)i1 * Q0 + i0]; }
+};
+struct BcFnSrc {
+  BcStage s;
+  __device__ __forceinline__ double operator()(int i0, int i1) const { return bc_stage_value(s, i0, i1); }
+};
+
+template <int ROWS, class Src>
+__global__ void __launch_bounds__(FACE_CHUNK) face_step1_kernel(const Src U, int Q0, int Q1,
                                                                  int i0_begin, int n0,
                                                                  const int *__restrict__ qs0,
                                                                  const double *__restrict__ w0T, int wmax0,
@@ -1746,8 +1759,7 @@ __global__ void __launch_bounds__(FACE_CHUNK) face_step1_kernel(const double *__
 #pragma unroll
   for (int r = 0; r < ROWS; ++r) {
     if (q1b + r < Q1) {
-      const double *src = U + (int64_t)(q1b + r) * Q0 + qa;
-      for (int e = threadIdx.x; e < nq; e += FACE_CHUNK) sh[r * qmax + e] = src[e];
+      for (int e = threadIdx.x; e < nq; e += FACE_CHUNK) sh[r * qmax + e] = U(qa + e, q1b + r);
     }
   }
   __syncthreads();
@@ -1782,8 +1794,8 @@ __device__ __forceinline__ int face_box_offset(int c, int p, int n) {
   return c < half ? 0 : min(n, c + half + 1) - p;
 }
 
-template <int P>
-__global__ void __launch_bounds__(512) face_cell_step1_kernel(const double *__restrict__ U, int Q0, int Q1, int rpb,
+template <int P, class Src>
+__global__ void __launch_bounds__(512) face_cell_step1_kernel(const Src U, int Q0, int Q1, int rpb,
                                                                int i0_begin, int n0, const int *__restrict__ crange,
                                                                const double *__restrict__ phi, int ncell_total,
                                                                int cell_begin, double *__restrict__ T) {
@@ -1795,12 +1807,11 @@ __global__ void __launch_bounds__(512) face_cell_step1_kernel(const double *__re
   const int r0 = blockIdx.x * rpb, r1 = min(Q1, r0 + rpb);
   for (int row = r0; row < r1; ++row) {
     __syncthreads();  // Phi ready / previous row's gather done
-    const double *u = U + (int64_t)row * Q0;
     for (int c = threadIdx.x; c < ncells; c += blockDim.x) {
       const int cat = face_category(cell_begin + c, P, ncell_total);
       double v[N1];
 #pragma unroll
-      for (int q = 0; q < N1; ++q) v[q] = u[c * N1 + q];
+      for (int q = 0; q < N1; ++q) v[q] = U(c * N1 + q, row);
       const double *ph = sphi + cat * N1 * N1;
 #pragma unroll
       for (int l = 0; l < N1; ++l) {
@@ -2122,6 +2133,51 @@ extern "C" hipError_t gdmk_launch_chol_lines(int p, double *v, int len, int64_t 
   return hipGetLastError();
 }
 
+template <class Src, class Step2>
+static hipError_t face_launch(const gdmk::FaceArgs &f, const Src &U, hipStream_t st, Step2 &step2) {
+  using namespace gdmk;
+  const int n0 = f.i0_end - f.i0_begin;
+  const size_t cell_lds = sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)f.Q0);
+  if (f.phi0 && cell_lds <= 48 * 1024) {
+    // cell form of step 1, then the usual step 2
+    const int rpb = 4;
+    dim3 g1c((f.Q1 + rpb - 1) / rpb);
+    if (f.phase != 2) switch (f.p) {
+#define GDM_FACE_CELL(PP)                                                                                            \
+  case PP:                                                                                                         \
+    hipLaunchKernelGGL((face_cell_step1_kernel<PP, Src>), g1c, dim3(512), cell_lds, st, U, f.Q0, f.Q1, rpb, f.i0_begin, \
+                       n0, f.crange0, f.phi0, f.ncell0_total, f.cell0_begin, f.T);                                 \
+    break;
+      GDM_FACE_CELL(1) GDM_FACE_CELL(3) GDM_FACE_CELL(5) GDM_FACE_CELL(7) GDM_FACE_CELL(9)
+#undef GDM_FACE_CELL
+      default: return hipErrorInvalidValue;
+    }
+    dim3 g2((n0 + 255) / 256, f.i1_end - f.i1_begin);
+    if (f.phase != 1) step2(g2);
+    return hipGetLastError();
+  }
+  // rows per workgroup: as many as fit 48 KiB of LDS (up to 4)
+  const size_t row_bytes = sizeof(double) * (size_t)f.qmax0;
+  const int rows = row_bytes * 4 <= 48 * 1024 ? 4 : (row_bytes * 2 <= 48 * 1024 ? 2 : 1);
+  if (row_bytes > 48 * 1024) return hipErrorInvalidValue;  // <= (FACE_CHUNK + 2p) (p + 1) doubles in practice
+  dim3 g1((n0 + FACE_CHUNK - 1) / FACE_CHUNK, (f.Q1 + rows - 1) / rows);
+  const size_t lds = row_bytes * rows;
+  if (f.phase == 2)
+    ;
+  else if (rows == 4)
+    hipLaunchKernelGGL((face_step1_kernel<4, Src>), g1, dim3(FACE_CHUNK), lds, st, U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
+                       f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
+  else if (rows == 2)
+    hipLaunchKernelGGL((face_step1_kernel<2, Src>), g1, dim3(FACE_CHUNK), lds, st, U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
+                       f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
+  else
+    hipLaunchKernelGGL((face_step1_kernel<1, Src>), g1, dim3(FACE_CHUNK), lds, st, U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
+                       f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
+  dim3 g2((n0 + 255) / 256, f.i1_end - f.i1_begin);
+  if (f.phase != 1) step2(g2);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) {
   using namespace gdmk;
   const int n0 = f.i0_end - f.i0_begin;
@@ -2141,47 +2197,13 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
       hipLaunchKernelGGL(face_step2_kernel<false>, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1,
                          f.w1, f.wmax1, f.dst, f.base, f.stride0, f.stride1, f.scale);
   };
-  const size_t cell_lds = sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)f.Q0);
-  if (f.phi0 && cell_lds <= 48 * 1024) {
-    // cell form of step 1, then the usual step 2
-    const int rpb = 4;
-    dim3 g1c((f.Q1 + rpb - 1) / rpb);
-    if (f.phase != 2) switch (f.p) {
-#define GDM_FACE_CELL(PP)                                                                                            \
-  case PP:                                                                                                         \
-    hipLaunchKernelGGL(face_cell_step1_kernel<PP>, g1c, dim3(512), cell_lds, st, f.U, f.Q0, f.Q1, rpb, f.i0_begin, \
-                       n0, f.crange0, f.phi0, f.ncell0_total, f.cell0_begin, f.T);                                 \
-    break;
-      GDM_FACE_CELL(1) GDM_FACE_CELL(3) GDM_FACE_CELL(5) GDM_FACE_CELL(7) GDM_FACE_CELL(9)
-#undef GDM_FACE_CELL
-      default: return hipErrorInvalidValue;
-    }
-    dim3 g2((n0 + 255) / 256, f.i1_end - f.i1_begin);
-    if (f.phase != 1) step2(g2);
-    return hipGetLastError();
+  if (f.stage) {
+    BcFnSrc s{*f.stage};
+    return face_launch(f, s, st, step2);
   }
-  dim3 b(256);
-  // rows per workgroup: as many as fit 48 KiB of LDS (up to 4)
-  const size_t row_bytes = sizeof(double) * (size_t)f.qmax0;
-  const int rows = row_bytes * 4 <= 48 * 1024 ? 4 : (row_bytes * 2 <= 48 * 1024 ? 2 : 1);
-  if (row_bytes > 48 * 1024) return hipErrorInvalidValue;  // <= (FACE_CHUNK + 2p) (p + 1) doubles in practice
-  dim3 g1((n0 + FACE_CHUNK - 1) / FACE_CHUNK, (f.Q1 + rows - 1) / rows);
-  const size_t lds = row_bytes * rows;
-  if (f.phase == 2)
-    ;
-  else if (rows == 4)
-    hipLaunchKernelGGL(face_step1_kernel<4>, g1, dim3(FACE_CHUNK), lds, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
-                       f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
-  else if (rows == 2)
-    hipLaunchKernelGGL(face_step1_kernel<2>, g1, dim3(FACE_CHUNK), lds, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
-                       f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
-  else
-    hipLaunchKernelGGL(face_step1_kernel<1>, g1, dim3(FACE_CHUNK), lds, st, f.U, f.Q0, f.Q1, f.i0_begin, n0, f.qs0,
-                       f.w0T, f.wmax0, f.ldw0, f.qmax0, f.T);
-  dim3 g2((n0 + 255) / 256, f.i1_end - f.i1_begin);
-  if (f.phase != 1) step2(g2);
-  return hipGetLastError();
+  return face_launch(f, BcArr{f.U, f.Q0}, st, step2);
 }
+
 
 extern "C" hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st) {
   using namespace gdmk;

@@ -29,6 +29,17 @@ struct BcFn {
   int kind, dim;
   double prm[12];
 };
+// the RK stage boundary values of one face, evaluated where they are read
+// (gdm_apply_bc_fn): y + alpha k with y = g(t_g), k = dg/dt(t_k); tab =
+// [2][kMaxFaces][3][ld][2] factor tables at t_g, then at t_k (bc_tables_kernel)
+struct BcStage {
+  static constexpr int kMaxFaces = 6;
+  BcGeom g;
+  BcFn f;
+  const double *tab;
+  int ld, face;
+  double alpha;
+};
 
 }  // namespace gdmk
 
@@ -54,4 +65,8 @@ hipError_t gdmk_launch_vmul(int64_t n, const double *w, const double *x, double 
 // tab: scratch of n_faces * 3 * ld * 2 doubles, ld >= max(Q0, Q1)
 hipError_t gdmk_launch_bc_eval(const gdmk::BcGeom &g, const gdmk::BcFn &f, double t, int derivative, double *out,
                                double *tab, int ld, hipStream_t st);
+// the factor tables of BcStage (kind 2; nothing to do otherwise): every face
+// at t_g and, with_k, at t_k, one launch; tab holds 2 * 6 * 3 * ld * 2 doubles
+hipError_t gdmk_launch_bc_tables(const gdmk::BcGeom &g, const gdmk::BcFn &f, double t_g, double t_k, int with_k,
+                                 double *tab, int ld, hipStream_t st);
 }

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cmath>
 
+#include "gdm_bcfn.h"
 #include "gdm_kernels.h"
 #include "gdm_rk.h"
 
@@ -78,26 +79,6 @@ __global__ void __launch_bounds__(256) rk_update_kernel(int64_t n, double beta, 
   }
 }
 
-namespace {
-
-// coordinate of quadrature point qi along face direction slot k (0 = t0, 1 = t1)
-__device__ __forceinline__ double slot_coord(const BcFace &F, const BcGeom &g, int k, int qi) {
-  const int e = F.dim_index[k];
-  const int n1 = g.p + 1;
-  const int c = F.cell_begin[k] + qi / n1, qq = qi - (qi / n1) * n1;
-  const double h = (g.hi[e] - g.lo[e]) / g.n_sub[e];
-  return g.lo[e] + (c + g.xq[qq]) * h;
-}
-
-// separable factor of GDM_FN_SINE_PRODUCT in direction e at coordinate x:
-// (s, c) = (sin, cos) of 2 pi k_e (x - a_e t) + phi_e
-__device__ __forceinline__ void sine_factor(const BcFn &f, int e, double x, double t, double &s, double &c) {
-  const double arg = 2.0 * M_PI * f.prm[3 + e] * (x - f.prm[e] * t) + f.prm[6 + e];
-  sincos(arg, &s, &c);
-}
-
-}  // namespace
-
 // Separable functions: per face, the 1D factors along t0 / t1 / the normal
 // are tabulated once (tab[slot][q] = (s, c); slot 2 = the normal coordinate),
 // so a boundary point costs two table reads and a few multiplies instead of
@@ -106,13 +87,27 @@ __device__ __forceinline__ void sine_factor(const BcFn &f, int e, double x, doub
 __global__ void __launch_bounds__(256) bc_table_kernel(BcGeom g, BcFace F, BcFn f, double t, double *tab, int ld) {
   const int slot = blockIdx.y;  // 0: t0, 1: t1, 2: normal
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < (slot < 2 ? F.Q[slot] : 1); q += gridDim.x * blockDim.x) {
-    double s = 1.0, c = 0.0;
-    if (slot < 2 && F.dim_index[slot] >= 0)
-      sine_factor(f, F.dim_index[slot], slot_coord(F, g, slot, q), t, s, c);
-    else if (slot == 2)
-      sine_factor(f, F.d, F.side ? g.hi[F.d] : g.lo[F.d], t, s, c);
+    double s, c;
+    bc_table_entry(g, F, f, t, slot, q, s, c);
     tab[((size_t)slot * ld + q) * 2] = s;
     tab[((size_t)slot * ld + q) * 2 + 1] = c;
+  }
+}
+
+// every face's tables at t_g (blockIdx.z < n_faces) and t_k (the rest) in
+// one launch: grid (x, 3 slots, n_faces or 2 n_faces); layout of BcStage::tab
+__global__ void __launch_bounds__(256) bc_tables_kernel(BcGeom g, BcFn f, double t_g, double t_k, double *tab,
+                                                        int ld) {
+  const int slot = blockIdx.y, z = blockIdx.z;
+  const int fi = z % g.n_faces, which = z / g.n_faces;
+  const BcFace &F = g.face[fi];
+  const double t = which ? t_k : t_g;
+  double *tb = tab + (size_t)(which * BcStage::kMaxFaces + fi) * 3 * ld * 2;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < (slot < 2 ? F.Q[slot] : 1); q += gridDim.x * blockDim.x) {
+    double s, c;
+    bc_table_entry(g, F, f, t, slot, q, s, c);
+    tb[((size_t)slot * ld + q) * 2] = s;
+    tb[((size_t)slot * ld + q) * 2 + 1] = c;
   }
 }
 
@@ -122,39 +117,7 @@ __global__ void __launch_bounds__(256) bc_face_kernel(BcGeom g, BcFace F, BcFn f
   const int i1 = blockIdx.y;
   const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (i0 >= F.Q[0]) return;
-  double *o = out + F.offset + (int64_t)i1 * F.Q[0] + i0;
-  if (f.kind == 0) {
-    *o = derivative ? 0.0 : f.prm[0];
-    return;
-  }
-  if (f.kind == 1) {  // cone max(0, r0 - |x - c|) (applications/advection/advection-app.cc:51-79), dg/dt = 0
-    if (derivative) {
-      *o = 0.0;
-      return;
-    }
-    double x[3] = {0.0, 0.0, 0.0};
-    x[F.d] = F.side ? g.hi[F.d] : g.lo[F.d];
-    if (F.dim_index[0] >= 0) x[F.dim_index[0]] = slot_coord(F, g, 0, i0);
-    if (F.dim_index[1] >= 0) x[F.dim_index[1]] = slot_coord(F, g, 1, i1);
-    double r2 = 0.0;
-    for (int d = 0; d < g.dim; ++d) r2 += (x[d] - f.prm[1 + d]) * (x[d] - f.prm[1 + d]);
-    *o = fmax(0.0, f.prm[0] - sqrt(r2));
-    return;
-  }
-  // kind 2: prod_d sin(.) over the dim directions; trivial slots hold (1, 0)
-  const double s0 = tab[2 * i0], c0 = tab[2 * i0 + 1];
-  const double s1 = tab[2 * ((size_t)ld + i1)], c1 = tab[2 * ((size_t)ld + i1) + 1];
-  const double sn = tab[2 * (size_t)2 * ld], cn = tab[2 * (size_t)2 * ld + 1];
-  if (!derivative) {
-    *o = s0 * s1 * sn;
-    return;
-  }
-  // d/dt: sum over directions of -2 pi k_e a_e cos(.) * the other sines
-  double r = 0.0;
-  if (F.dim_index[0] >= 0) r += -2.0 * M_PI * f.prm[3 + F.dim_index[0]] * f.prm[F.dim_index[0]] * c0 * s1 * sn;
-  if (F.dim_index[1] >= 0) r += -2.0 * M_PI * f.prm[3 + F.dim_index[1]] * f.prm[F.dim_index[1]] * s0 * c1 * sn;
-  r += -2.0 * M_PI * f.prm[3 + F.d] * f.prm[F.d] * s0 * s1 * cn;
-  *o = r;
+  out[F.offset + (int64_t)i1 * F.Q[0] + i0] = bc_point(g, F, f, tab, ld, i0, i1, derivative);
 }
 
 // Periodicity constraints of System::make_periodicity_constraints
@@ -341,6 +304,15 @@ extern "C" hipError_t gdmk_launch_bc_eval(const gdmk::BcGeom &g, const gdmk::BcF
     hipLaunchKernelGGL(gdmk::bc_face_kernel, dim3((unsigned)((F.Q[0] + 255) / 256), (unsigned)F.Q[1]), dim3(256), 0,
                        st, g, F, f, t, derivative, tab + (size_t)fi * 3 * ld * 2, ld, out);
   }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gdmk_launch_bc_tables(const gdmk::BcGeom &g, const gdmk::BcFn &f, double t_g, double t_k,
+                                            int with_k, double *tab, int ld, hipStream_t st) {
+  if (f.kind != 2 || g.n_faces <= 0) return hipSuccess;
+  if (g.n_faces > gdmk::BcStage::kMaxFaces) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gdmk::bc_tables_kernel, dim3((unsigned)((ld + 255) / 256), 3, (unsigned)(g.n_faces * (with_k ? 2 : 1))),
+                     dim3(256), 0, st, g, f, t_g, t_k, tab, ld);
   return hipGetLastError();
 }
 

@@ -192,6 +192,16 @@ class GdmOperator:
                                          _ptr(out)), "gdm_eval_boundary")
         return out
 
+    def apply_bc_fn(self, src_local, dst_owned, fn_kind, params, t_g, alpha=0.0, t_k=0.0):
+        """apply() with the stage boundary values g(t_g) + alpha dg/dt(t_k) of a
+        built-in function evaluated inside the face kernels (gdm_apply_bc_fn):
+        the same bits as eval_boundary + rk_update + apply(bc_values)"""
+        self._check_sizes(src_local, dst_owned)
+        prm = (ctypes.c_double * max(len(params), 1))(*[float(v) for v in params])
+        check(self.lib.gdm_apply_bc_fn(self.h, _ptr(src_local), _ptr(dst_owned), int(fn_kind), prm, len(params),
+                                       float(t_g), float(alpha), float(t_k)), "gdm_apply_bc_fn")
+        return dst_owned
+
     def mass_solve_slab(self, rhs_owned, x_owned):
         """Distributed exact mass inverse, step 1: the slab-local solve
         (gdm_mass_solve_slab).  Then exchange the ghost planes of the local

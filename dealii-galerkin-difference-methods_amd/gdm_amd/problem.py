@@ -16,7 +16,12 @@ and nothing crosses PCIe inside the loop.  Block(0) of the advection problem
 is g(t_n) at the start of every step (initialize_time_step,
 advection/stiffness.h:181-194) and dg/dt at the stage times
 (stiffness.h:286-289), both evaluated on the device for the built-in
-boundary functions (gdm_eval_boundary).
+boundary functions.  By default block(0) is not stored at all: stage s reads
+y0 + h a_{s,s-1} k_{s-1} = g(t_n) + h a dg/dt(t_n + c_{s-1} h), which the
+face kernels evaluate where they read it (gdm_apply_bc_fn, the same bits as
+gdm_eval_boundary + gdm_vec_rk_update); block(0) after a step is never read
+by the reference (initialize_time_step overwrites it, problem.h:88-90).
+carry_bc=True keeps the explicit block(0) vectors (gdm_eval_boundary).
 """
 from ._capi import GdmError
 
@@ -111,10 +116,11 @@ class AdvectionProblem:
     """advection problem.h:31-102 on one rank with a built-in boundary
     function (gdm_fn_kind) for g and dg/dt."""
 
-    def __init__(self, op, fn_kind, fn_params):
+    def __init__(self, op, fn_kind, fn_params, carry_bc=False):
         if op.mesh.n_ranks != 1:
             raise GdmError("AdvectionProblem: single-rank driver")
         self.op, self.fn, self.prm = op, int(fn_kind), list(fn_params)
+        self.carry_bc = bool(carry_bc)  # False: self.bc is not maintained
         nb = max(op.n_bc_points, 1)
         import torch
 
@@ -140,6 +146,19 @@ class AdvectionProblem:
 
     def step(self, t, h):
         op = self.op
+        if not self.carry_bc:
+            # block(0) evaluated in the face kernels: stage s reads g(t) + alpha dg/dt(t_k)
+            y, acc, Y, k = self.u, self._acc[1], self._Y[1], self._k[1]
+            stage = y
+            for s in range(4):
+                alpha, t_k = (0.0, t) if s == 0 else (h * RK4_A[s - 1], t + RK4_C[s - 1] * h)
+                op.apply_bc_fn(stage, k, self.fn, self.prm, t, alpha, t_k)
+                op.mass_solve(k, k)
+                last = s == 3
+                op.rk_update(h * RK4_B[s], k, y if s == 0 else acc, y if last else acc,
+                             0.0 if last else h * RK4_A[s], None if last else y, None if last else Y)
+                stage = Y
+            return
         self.initialize_time_step(t)
         y = (self.bc, self.u)
         acc, Y, k = self._acc, self._Y, self._k

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 10
+#define GDM_HIP_ABI_VERSION 11
 
 enum gdm_status {
   GDM_OK = 0,
@@ -288,6 +288,19 @@ int gdm_vec_rk_update(gdm_op *op, int64_t n, double beta, const double *k, const
                       double alpha, const double *y, double *Y);
 int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_params, double t, int derivative,
                       double *bc_values);
+/* gdm_apply_bc_fn: gdm_apply (stencil + inflow boundary term) with the stage
+ * boundary values evaluated inside the face kernels instead of read from a
+ * bc_values vector: BC = g(t_g) + alpha dg/dt(t_k) (alpha = 0: g(t_g)), the
+ * same bits as gdm_eval_boundary(g, t_g) / (dg/dt, t_k) followed by
+ * gdm_vec_rk_update's Y = y + alpha k.  This is block(0) of the reference's
+ * RK stages (advection/problem.h:62-94 with initialize_time_step,
+ * stiffness.h:181-194, and the dg/dt stage block, stiffness.h:286-289) for
+ * the classic RK4 tableau, where stage s >= 1 reads y0 + h a_{s,s-1} k_{s-1}:
+ * the block(0) vectors and their stage updates disappear (block(0) after a
+ * step is never read: initialize_time_step overwrites it, problem.h:88-90).
+ * Advection operators; fn_kind / params as gdm_eval_boundary. */
+int gdm_apply_bc_fn(gdm_op *op, const double *src_local, double *dst_owned, int fn_kind, const double *params,
+                    int n_params, double t_g, double alpha, double t_k);
 
 /* ----------------------------------------------------------------------
  * Postprocess on the device
