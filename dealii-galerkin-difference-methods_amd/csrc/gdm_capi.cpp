@@ -1830,6 +1830,34 @@ int gdm_apply_bc_fn(gdm_op *op, const double *src_local, double *dst_owned, int 
   GDM_GUARD_END
 }
 
+int gdm_add_boundary_fn(gdm_op *op, double *dst_owned, int fn_kind, const double *params, int n_params, double t_g,
+                        double alpha, double t_k) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_bc_points > 0 && !dst_owned) return fail(GDM_ERR_ARG, "NULL vector");
+  if (op->kind != GDM_OP_ADVECTION) return fail(GDM_ERR_UNSUPPORTED, "gdm_add_boundary_fn: advection operators only");
+  if (int rc = check_bc_fn(op, fn_kind, params, n_params)) return rc;
+  if (op->layout.n_bc_points == 0) return GDM_OK;
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  gdmk::BcStage stage{};
+  int ld = 1;
+  build_bc_fn(op, fn_kind, params, n_params, stage.g, stage.f, ld);
+  if (!op->bc_stage_tab || op->bc_stage_ld < ld) {
+    std::vector<double> zero((size_t)2 * gdmk::BcStage::kMaxFaces * 3 * ld * 2, 0.0);
+    op->bc_stage_tab = keep(op, dev_upload(zero));
+    op->bc_stage_ld = ld;
+  }
+  stage.tab = op->bc_stage_tab;
+  stage.ld = op->bc_stage_ld;
+  stage.alpha = alpha;
+  hip_check(gdmk_launch_bc_tables(stage.g, stage.f, t_g, t_k, alpha != 0.0 ? 1 : 0, op->bc_stage_tab, stage.ld,
+                                  op->stream),
+            "bc tables");
+  launch_boundary_data(op, nullptr, dst_owned, 0, nullptr, &stage);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
 int gdm_error_norms(gdm_op *op, const double *u_local, int fn_kind, const double *params, int n_params, double t,
                     double *cell_errors, double *norms_host) {
   if (!op || !norms_host) return fail(GDM_ERR_ARG, "NULL argument");

@@ -138,6 +138,7 @@ def load():
         "gdm_vec_rk_update": [P, i64, d, P, P, P, d, P, P],
         "gdm_eval_boundary": [P, i32, P, i32, d, i32, P],
         "gdm_apply_bc_fn": [P, P, P, i32, P, i32, d, d, d],
+        "gdm_add_boundary_fn": [P, P, i32, P, i32, d, d, d],
         "gdm_error_norms": [P, P, i32, P, i32, d, P, P],
         "gdm_mass_spike_eps": [P, P],
         "gdm_mass_solve_slab": [P, P, P],

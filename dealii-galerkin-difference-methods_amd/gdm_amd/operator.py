@@ -202,6 +202,14 @@ class GdmOperator:
                                        float(t_g), float(alpha), float(t_k)), "gdm_apply_bc_fn")
         return dst_owned
 
+    def add_boundary_fn(self, dst_owned, fn_kind, params, t_g, alpha=0.0, t_k=0.0):
+        """add_boundary_data() with the stage boundary values of apply_bc_fn (gdm_add_boundary_fn)"""
+        self._check_sizes(None, dst_owned)
+        prm = (ctypes.c_double * max(len(params), 1))(*[float(v) for v in params])
+        check(self.lib.gdm_add_boundary_fn(self.h, _ptr(dst_owned), int(fn_kind), prm, len(params), float(t_g),
+                                           float(alpha), float(t_k)), "gdm_add_boundary_fn")
+        return dst_owned
+
     def mass_solve_slab(self, rhs_owned, x_owned):
         """Distributed exact mass inverse, step 1: the slab-local solve
         (gdm_mass_solve_slab).  Then exchange the ghost planes of the local

@@ -11,7 +11,9 @@
 // values after STEPS RK4 steps to OUT (raw little-endian doubles, reference
 // global order) and prints one line per step with |u|_2.  DEVBC = 1 evaluates
 // g and dg/dt on the device (GDM_FN_SINE_PRODUCT with the same parameters)
-// instead of the host callbacks.  NRANKS > 1 runs the multi-rank path: one
+// instead of the host callbacks, with the stage values of block(0) evaluated
+// inside the face kernels (Parameters::boundary_in_faces); DEVBC = 2 the same
+// function with block(0) stored and RK-updated.  NRANKS > 1 runs the multi-rank path: one
 // thread per rank (z-slabs of system.h:720-757, all on DEVICE), ghost planes
 // and dots through GDM::HIP::ThreadGroup (an MPI communicator's role), the
 // distributed exact mass inverse (SPIKE) when the slabs are thick enough, else
@@ -77,6 +79,7 @@ GDM::HIP::Parameters<dim> make_params(int p, int n, double cfl, int device, int 
   if (devbc) {
     params.boundary_function = GDM_FN_SINE_PRODUCT;
     params.boundary_function_params = {kA[0], kA[1], kA[2], 1.0, 1.0, 1.0, 0.0, 0.3, 0.6};
+    params.boundary_in_faces = devbc != 2;
   }
   return params;
 }

@@ -72,6 +72,12 @@ struct Parameters {
   // upload (the reference's behaviour, a PCIe copy per stage).
   int boundary_function = -1;
   std::vector<double> boundary_function_params;
+  // with a built-in boundary function: evaluate the stage values of block(0)
+  // (g(t_n) + h a_{s,s-1} dg/dt) inside the face kernels (gdm_apply_bc_fn /
+  // gdm_add_boundary_fn) instead of storing and RK-updating block(0); the
+  // same bits for block(1); block(0) of the solution is then not maintained
+  // (initialize_time_step overwrites it every step, problem.h:88-90)
+  bool boundary_in_faces = true;
 };
 
 // A device buffer of doubles allocated through the engine (gdm_malloc).
@@ -293,21 +299,49 @@ class StiffnessMatrixOperator {
       return;
     }
     set_boundary(vec_rhs.block(0), time, 1);
+    apply_planes_overlapped(vec_rhs.block(1), src.block(1), comm);
+    if (layout.n_bc_points > 0)
+      check(gdm_add_boundary_data(op, src.block(0).get_values(), owned(vec_rhs.block(1))), "gdm_add_boundary_data");
+  }
+  // the volume term of every owned plane, the planes that need no ghosts while
+  // the exchange of u's ghost planes is in flight
+  void apply_planes_overlapped(DeviceVector &rhs_block1, DeviceVector &u_vec, Communicator &comm) const {
     const int p = layout.halo_depth, pb = (int)layout.owned_plane_begin, pe = (int)layout.owned_plane_end;
     const int lo = pb + (layout.ghost_planes_below ? p : 0), hi = pe - (layout.ghost_planes_above ? p : 0);
-    const double *u = src.block(1).get_values();
-    double *dst = owned(vec_rhs.block(1));
-    comm.begin_update_ghost_values(op, src.block(1));
+    const double *u = u_vec.get_values();
+    double *dst = owned(rhs_block1);
+    comm.begin_update_ghost_values(op, u_vec);
     if (hi > lo) check(gdm_apply_planes(op, u, dst, lo, hi), "gdm_apply_planes");
-    comm.end_update_ghost_values(op, src.block(1));
+    comm.end_update_ghost_values(op, u_vec);
     if (hi <= lo) {
       check(gdm_apply_planes(op, u, dst, pb, pe), "gdm_apply_planes");
     } else {
       if (lo > pb) check(gdm_apply_planes(op, u, dst, pb, lo), "gdm_apply_planes");
       if (pe > hi) check(gdm_apply_planes(op, u, dst, hi, pe), "gdm_apply_planes");
     }
-    if (layout.n_bc_points > 0)
-      check(gdm_add_boundary_data(op, src.block(0).get_values(), dst), "gdm_add_boundary_data");
+  }
+
+  // block(0) from the built-in function inside the face kernels
+  bool boundary_in_faces() const { return bc_fn >= 0 && layout.n_bc_points > 0; }
+  // compute_rhs's block(1) with the stage boundary values g(t_g) + alpha
+  // dg/dt(t_k) evaluated where the face kernels read them (gdm_apply_bc_fn)
+  void compute_rhs_fn(DeviceVector &rhs_block1, const DeviceVector &u, double t_g, double alpha, double t_k) const {
+    check(gdm_apply_bc_fn(op, u.get_values(), owned(rhs_block1), bc_fn, bc_fn_params.data(),
+                          (int)bc_fn_params.size(), t_g, alpha, t_k),
+          "gdm_apply_bc_fn");
+  }
+  // compute_rhs_overlapped with the boundary values of compute_rhs_fn
+  void compute_rhs_fn_overlapped(DeviceVector &rhs_block1, DeviceVector &u, double t_g, double alpha, double t_k,
+                                 Communicator &comm) const {
+    if (dim != 3) {
+      comm.update_ghost_values(op, u);
+      compute_rhs_fn(rhs_block1, u, t_g, alpha, t_k);
+      return;
+    }
+    apply_planes_overlapped(rhs_block1, u, comm);
+    check(gdm_add_boundary_fn(op, owned(rhs_block1), bc_fn, bc_fn_params.data(), (int)bc_fn_params.size(), t_g,
+                              alpha, t_k),
+          "gdm_add_boundary_fn");
   }
 
   gdm_op *handle() const { return op; }
@@ -526,8 +560,19 @@ class AdvectionProblem {
     stiffness_matrix_operator.initialize_dof_vector(stage);
     if (params.n_ranks != 1) rhs_tmp.reinit(stiffness_matrix_operator.handle(), stiffness_matrix_operator.get_layout().n_owned);
     use_spike = params.n_ranks != 1 && mass_matrix_operator.spike_available();
+    const bool in_faces = params.boundary_in_faces && stiffness_matrix_operator.boundary_in_faces();
+    // stage boundary values inside the face kernels: g(t0) + alpha dg/dt(t_k)
+    double t0 = 0.0, bc_alpha = 0.0, bc_tk = 0.0;
     const auto fu_rhs = [&](double time, BlockVector &y, BlockVector &result) {
-      if (params.n_ranks != 1 && params.overlap_exchange) {
+      if (in_faces) {
+        if (params.n_ranks != 1 && params.overlap_exchange) {
+          stiffness_matrix_operator.compute_rhs_fn_overlapped(result.block(1), y.block(1), t0, bc_alpha, bc_tk,
+                                                              *comm);
+        } else {
+          if (params.n_ranks != 1) comm->update_ghost_values(stiffness_matrix_operator.handle(), y.block(1));
+          stiffness_matrix_operator.compute_rhs_fn(result.block(1), y.block(1), t0, bc_alpha, bc_tk);
+        }
+      } else if (params.n_ranks != 1 && params.overlap_exchange) {
         stiffness_matrix_operator.compute_rhs_overlapped(result, y, time, *comm);
       } else {
         if (params.n_ranks != 1) comm->update_ghost_values(stiffness_matrix_operator.handle(), y.block(1));
@@ -548,11 +593,15 @@ class AdvectionProblem {
     DiscreteTime time(params.start_t, params.end_t, delta_t);
     unsigned int n = 0;
     while (!time.is_at_end() && n < max_steps) {
-      stiffness_matrix_operator.initialize_time_step(solution, time.get_current_time());  // evaluate bc
-      const double t0 = time.get_current_time(), h = time.get_next_step_size();
+      t0 = time.get_current_time();
+      const double h = time.get_next_step_size();
+      if (!in_faces) stiffness_matrix_operator.initialize_time_step(solution, t0);  // evaluate bc
       for (int s = 0; s < 4; ++s) {
+        // stage s reads block(0) = g(t0) + h a_{s,s-1} dg/dt(t0 + c_{s-1} h)
+        bc_alpha = s == 0 ? 0.0 : h * ClassicRK4::a[s];
+        bc_tk = s == 0 ? t0 : t0 + ClassicRK4::c[s - 1] * h;
         fu_rhs(t0 + ClassicRK4::c[s] * h, s == 0 ? solution : stage, k);  // ghosts of the stage exchanged
-        for (unsigned int bl = 0; bl < 2; ++bl)
+        for (unsigned int bl = in_faces ? 1 : 0; bl < 2; ++bl)
           rk4_stage_update(s, h, k.block(bl), solution.block(bl), acc.block(bl), stage.block(bl));
       }
       time.advance_time();

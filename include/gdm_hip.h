@@ -301,6 +301,10 @@ int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_param
  * Advection operators; fn_kind / params as gdm_eval_boundary. */
 int gdm_apply_bc_fn(gdm_op *op, const double *src_local, double *dst_owned, int fn_kind, const double *params,
                     int n_params, double t_g, double alpha, double t_k);
+/* gdm_add_boundary_fn: gdm_add_boundary_data with the stage boundary values
+ * of gdm_apply_bc_fn (the inflow term alone, after gdm_apply_planes) */
+int gdm_add_boundary_fn(gdm_op *op, double *dst_owned, int fn_kind, const double *params, int n_params, double t_g,
+                        double alpha, double t_k);
 
 /* ----------------------------------------------------------------------
  * Postprocess on the device

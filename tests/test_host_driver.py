@@ -82,6 +82,22 @@ def test_driver_fails_loudly_without_gpu(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dim,p,n,steps,ranks", [(2, 5, 24, 3, 1), (3, 5, 12, 2, 1), (3, 5, 24, 2, 2)])
+def test_driver_boundary_in_faces_bitwise(tmp_path, dim, p, n, steps, ranks):
+    """devbc = 1 (block(0) stage values evaluated in the face kernels,
+    gdm_apply_bc_fn / gdm_add_boundary_fn) and devbc = 2 (block(0) stored and
+    RK-updated, gdm_eval_boundary + gdm_vec_rk_update) give the same bits"""
+    u = []
+    for devbc in (1, 2):
+        out = tmp_path / ("u%d.bin" % devbc)
+        r = subprocess.run([APP, str(dim), str(p), str(n), str(steps), "0.1", str(out), "0", str(devbc), str(ranks)],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        u.append(np.fromfile(out, dtype=np.float64))
+    assert u[0].size > 0 and np.array_equal(u[0], u[1])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dim,p,n,steps", [(1, 3, 40, 4), (2, 5, 24, 3), (3, 3, 10, 2), (3, 5, 12, 2)])
 @pytest.mark.parametrize("devbc", [0, 1])
 def test_driver_rk4_matches_oracle(tmp_path, dim, p, n, steps, devbc):
