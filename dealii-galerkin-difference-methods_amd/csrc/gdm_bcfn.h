@@ -73,7 +73,7 @@ __device__ __forceinline__ double bc_stage_value(const BcStage &s, int i0, int i
   const double y = bc_point(s.g, F, s.f, s.tab + (size_t)s.face * 3 * s.ld * 2, s.ld, i0, i1, 0);
   if (s.alpha == 0.0) return y;
   const double k = bc_point(s.g, F, s.f, s.tab + (size_t)(BcStage::kMaxFaces + s.face) * 3 * s.ld * 2, s.ld, i0, i1, 1);
-  return y + s.alpha * k;
+  return fma(s.alpha, k, y);
 }
 
 }  // namespace gdmk

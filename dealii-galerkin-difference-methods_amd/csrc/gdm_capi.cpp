@@ -1068,9 +1068,13 @@ void build_spike(gdm_op *op) {
 #ifndef GDM_MASS_X_STRIDED
 #define GDM_MASS_X_STRIDED 0
 #endif
-void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, const LineTables *part) {
+// rk (single rank): the RK stage update of gdm_mass_solve_rk fused into the
+// last pass when that is the unsegmented v3 x pass; returns whether it was
+// (else x_owned holds M^-1 rhs and the caller updates)
+bool mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, const LineTables *part,
+                       const gdmk::RkOut *rk = nullptr) {
   const int64_t n = op->layout.n_owned;
-  if (n <= 0) return;
+  if (n <= 0) return false;
   int64_t K[3] = {op->K[0], op->K[1], op->K[2]};
   LineTables tab[3];
   for (int ax = 0; ax < 3; ++ax) {
@@ -1148,6 +1152,12 @@ void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
       }
     }
     const LineTables &t = tab[q.ax];
+    if (rk && i == np - 1 && !segmented && !part && q.dir_kind == 0 && use_v3(q, in, in)) {
+      const hipError_t e = gdmk_launch_mass3_rk(op->p, in, (int)q.len, q.n_lines, t.l3, t.u3, t.d3, t.cst.data(),
+                                                t.row_lo, t.row_hi, *rk, op->stream);
+      if (e == hipSuccess) return true;
+      if (e != hipErrorNotSupported) hip_check(e, "mass x + rk update");
+    }
     if (use_v3(q, in, out))
       hip_check(gdmk_launch_mass3(op->p, q.dir_kind, in, out, (int)q.len, q.stride, q.n_lines, q.A, q.B, t.l3, t.u3,
                                   t.d3, t.cst.data(), t.row_lo, t.row_hi, segmented ? 1 : 0, op->stream),
@@ -1160,6 +1170,7 @@ void mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
   }
   if (in != x_owned)
     hip_check(hipMemcpyAsync(x_owned, in, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+  return false;
 }
 
 }  // namespace
@@ -1482,6 +1493,23 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned) {
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   mass_solve_passes(op, rhs_owned, x_owned, nullptr);
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_mass_solve_rk(gdm_op *op, double *rhs_owned, double beta, const double *acc_in, double *acc_out,
+                      double alpha, const double *y, double *Y) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->mesh.n_ranks != 1) return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_rk: single rank");
+  if (op->mesh.periodic) return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_rk: periodic constraints");
+  if (!rhs_owned || !acc_in || !acc_out || (Y && !y)) return fail(GDM_ERR_ARG, "NULL vector");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  const gdmk::RkOut rk{acc_in, acc_out, y, Y, beta, alpha};
+  if (!mass_solve_passes(op, rhs_owned, rhs_owned, nullptr, &rk))
+    hip_check(gdmk_launch_rk_update(op->layout.n_owned, beta, rhs_owned, acc_in, acc_out, alpha, Y ? y : nullptr, Y,
+                                    op->stream),
+              "rk_update");
   return GDM_OK;
   GDM_GUARD_END
 }

@@ -86,6 +86,18 @@ struct FaceArgs {
               // 3: both steps into G (G = scale s), 4: dst += G
 };
 
+// The RK stage update fused into the mass inverse's x pass (gdmk_launch_mass3_rk):
+// the line solve's result k is not stored; acc_out = acc_in + beta k and, with
+// Y, Y = y + alpha k (gdm_vec_rk_update's arithmetic) are.  acc_in may alias
+// acc_out; Y may be NULL.  Element offsets relative to each pointer = k's.
+struct RkOut {
+  const double *acc_in;
+  double *acc_out;
+  const double *y;
+  double *Y;
+  double beta, alpha;
+};
+
 constexpr int FACE_CHUNK = 256;  // t0 nodes per workgroup of the face row kernel
 
 // hipFuncAttributeMaxDynamicSharedMemorySize is a per-device property of a
@@ -127,6 +139,12 @@ hipError_t gdmk_launch_mass3(int p, int dir_kind, const double *src, double *dst
                              int64_t n_lines, int64_t A, int64_t B, const double *lrow, const double *urow,
                              const double *invd, const double *cst, int row_lo, int row_hi, int allow_segments,
                              hipStream_t st);
+// the x pass (dir_kind 0, contiguous lines, no segments) with the RK update
+// fused into its store; hipErrorNotSupported when the v3 x pass cannot run
+// unsegmented for this shape (the caller then solves and updates separately)
+hipError_t gdmk_launch_mass3_rk(int p, const double *src, int len, int64_t n_lines, const double *lrow,
+                                const double *urow, const double *invd, const double *cst, int row_lo, int row_hi,
+                                const gdmk::RkOut &rk, hipStream_t st);
 hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st);
 hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st);
 hipError_t gdmk_launch_dot(int64_t n, const double *x, const double *y, double *partial, int n_partial, double *out,

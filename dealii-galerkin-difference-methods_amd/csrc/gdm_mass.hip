@@ -627,15 +627,22 @@ __global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel
 // chunk staged in registers ran all four SIMDs but measured 2-9 % slower on
 // the MI355X, profiles/r3i/ab_mass.txt.)
 // Requires len even and 16-B aligned src / dst (host-checked).
-template <int P, bool SEG>
+// RKM (the RK stage update fused into the store, gdmk_launch_mass3_rk): 0 = store
+// the solution into dst; 1 = acc_out = acc_in + beta k; 2 = also Y = y + alpha
+// k.  acc_in / y of the chunk to be stored are loaded into registers before the
+// chunk's arithmetic (their latency hides behind it); k never reaches memory.
+template <int P, bool SEG, int RKM = 0>
 __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, double *dst, int len, int64_t n_lines,
                                                         const double *__restrict__ lrow,
                                                         const double *__restrict__ urow,
                                                         const double *__restrict__ invd, const Cst3<P> k,
-                                                        int seg_chunks) {
+                                                        int seg_chunks, const RkOut rk) {
   using R = Ring3<P>;
   using G = Geo3<P>;
   constexpr int C = R::C, UPR = G::UPR, QL = G::QL;
+  static_assert(RKM == 0 || !SEG, "the fused RK update runs unsegmented");
+  // stores in flight after the last load of an iteration (the loop-top wait)
+  constexpr int NST = UPR * (RKM == 2 ? 2 : 1);
   extern __shared__ __attribute__((aligned(16))) char smem3[];
   ldouble2 *tile0 = (ldouble2 *)smem3;
   ldouble2 *tile1 = tile0 + G::TILE;
@@ -684,6 +691,25 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
+  // the RK operands of the chunk at `base` (RKM > 0), fetched one chunk of
+  // arithmetic ahead of their use
+  dpair pa[RKM ? UPR : 1], py[RKM == 2 ? UPR : 1];
+  const int64_t obase = l0 * len;
+  auto prefetch = [&](int base) {
+    if constexpr (RKM > 0) {
+      const int last_pair = min(C / 2, (len - base) / 2) - 1;
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int q = 0; q < UPR; ++q) {
+        const int u = q * 64 + ln;
+        const int row = min(u / UPR, nl - 1), pair = min(u % UPR, last_pair);
+        const int64_t e = obase + (int64_t)row * len + base + 2 * pair;
+        pa[q] = __builtin_nontemporal_load(reinterpret_cast<const dpair *>(rk.acc_in + e));
+        if constexpr (RKM == 2) py[q] = __builtin_nontemporal_load(reinterpret_cast<const dpair *>(rk.y + e));
+      }
+    }
+  };
   auto store = [&](const ldouble2 *t, int base) {
     const int last_pair = min(C / 2, (len - base) / 2) - 1;  // >= 0: base < len, len even
     int ln = lane;
@@ -694,11 +720,23 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
       const int u = q * 64 + ln;
       const int row = min(u / UPR, nl - 1), pair = min(u % UPR, last_pair);
       const dpair v = t[row * UPR + pair];
+      if constexpr (RKM > 0) {
+        // gdm_vec_rk_update (rk_update2_kernel): acc_in + beta k, y + alpha k, one FMA each
+        const int64_t e = obase + (int64_t)row * len + base + 2 * pair;
+        const dpair bv = {rk.beta, rk.beta};
+        __builtin_nontemporal_store(__builtin_elementwise_fma(bv, v, pa[q]),
+                                    reinterpret_cast<dpair *>(rk.acc_out + e));
+        if constexpr (RKM == 2) {
+          const dpair av = {rk.alpha, rk.alpha};
+          __builtin_nontemporal_store(__builtin_elementwise_fma(av, v, py[q]), reinterpret_cast<dpair *>(rk.Y + e));
+        }
+      } else {
 #if GDM_MASS_ST_CPOL
-      __builtin_nontemporal_store(v, reinterpret_cast<dpair *>(dbase + (int64_t)row * len + base + 2 * pair));
+        __builtin_nontemporal_store(v, reinterpret_cast<dpair *>(dbase + (int64_t)row * len + base + 2 * pair));
 #else
-      *reinterpret_cast<dpair *>(dbase + (int64_t)row * len + base + 2 * pair) = v;
+        *reinterpret_cast<dpair *>(dbase + (int64_t)row * len + base + 2 * pair) = v;
 #endif
+      }
     }
     GDM_FENCE();
   };
@@ -725,6 +763,7 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
   for (int c = c0 + 1;; c += 2) {
     // ---- chunk c: tile1, ring h1; chunk c - 1 in h0 (its input tile0 is free) ----
     if (c * C >= len) {
+      if (c - 1 >= cb) prefetch((c - 1) * C);
       r.template bwd<false, GDM_MASS_EDGE_MODE>(h0, h1, (c - 1) * C);
       if (c - 1 >= cb) {
         write_row(tile0, h0);
@@ -735,8 +774,9 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
     if (c == c0 + 1 || c - 2 < cb)
       GDM_WAIT_VMCNT(0);  // only DMA(c) is in flight (no stores were issued after it)
     else
-      GDM_WAIT_VMCNT(UPR);  // DMA(c) retired; the stores issued after it may be in flight
+      GDM_WAIT_VMCNT(NST);  // DMA(c) retired (RKM: so did the loads after it); the stores may be in flight
     if ((c + 1) * C < len && (!SEG || c + 1 <= ce)) dma(tile0, (c + 1) * C);
+    if (c - 1 >= cb) prefetch((c - 1) * C);
     open_row(tile1);
     r.step(h1, h0, c, get, none);
     if (c - 1 >= cb) {
@@ -746,6 +786,7 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
     if (SEG && c == ce) break;  // chunk ce was the backward warm-up
     // ---- chunk c + 1: tile0, ring h0; chunk c in h1 ----
     if ((c + 1) * C >= len) {
+      prefetch(c * C);
       r.template bwd<false, GDM_MASS_EDGE_MODE>(h1, h0, c * C);
       write_row(tile1, h1);
       store(tile1, c * C);
@@ -754,8 +795,9 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
     if (c - 1 < cb)
       GDM_WAIT_VMCNT(0);
     else
-      GDM_WAIT_VMCNT(UPR);
+      GDM_WAIT_VMCNT(NST);
     if ((c + 2) * C < len && (!SEG || c + 2 <= ce)) dma(tile1, (c + 2) * C);
+    prefetch(c * C);
     open_row(tile0);
     r.step(h0, h1, c + 1, get, none);
     write_row(tile0, h1);
@@ -817,10 +859,10 @@ hipError_t launch_mass3_p(int dir_kind, const double *src, double *dst, int len,
     static_assert(lds <= 64 * 1024, "mass3_rows_kernel LDS above the default limit");
     if (seg_chunks)
       hipLaunchKernelGGL((mass3_rows_kernel<P, true>), dim3(grid, n_segs), dim3(64), lds, st, src, dst, len, n_lines,
-                         lrow, urow, invd, k, seg_chunks);
+                         lrow, urow, invd, k, seg_chunks, RkOut{});
     else
       hipLaunchKernelGGL((mass3_rows_kernel<P, false>), dim3(grid), dim3(64), lds, st, src, dst, len, n_lines, lrow,
-                         urow, invd, k, 0);
+                         urow, invd, k, 0, RkOut{});
   } else {
     if (seg_chunks)
       hipLaunchKernelGGL((mass3_strided_kernel<P, true>), dim3(grid, n_segs), dim3(64), 0, st, src, dst, len, stride,
@@ -832,9 +874,48 @@ hipError_t launch_mass3_p(int dir_kind, const double *src, double *dst, int len,
   return hipGetLastError();
 }
 
+template <int P>
+hipError_t launch_mass3_rk_p(const double *src, int len, int64_t n_lines, const double *lrow, const double *urow,
+                             const double *invd, const double *cst, int row_lo, int row_hi, const RkOut &rk,
+                             hipStream_t st) {
+  Cst3<P> k;
+  for (int q = 0; q < P; ++q) {
+    k.l[q] = cst[q];
+    k.u[q] = cst[P + q];
+  }
+  k.d = cst[2 * P];
+  k.row_lo = row_lo;
+  k.row_hi = row_hi;
+  const unsigned grid = (unsigned)((n_lines + 63) / 64);
+  constexpr size_t lds = Geo3<P>::lds_bytes();
+  if (rk.Y)
+    hipLaunchKernelGGL((mass3_rows_kernel<P, false, 2>), dim3(grid), dim3(64), lds, st, src, nullptr, len, n_lines,
+                       lrow, urow, invd, k, 0, rk);
+  else
+    hipLaunchKernelGGL((mass3_rows_kernel<P, false, 1>), dim3(grid), dim3(64), lds, st, src, nullptr, len, n_lines,
+                       lrow, urow, invd, k, 0, rk);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 }  // namespace gdmk
+
+extern "C" hipError_t gdmk_launch_mass3_rk(int p, const double *src, int len, int64_t n_lines, const double *lrow,
+                                          const double *urow, const double *invd, const double *cst, int row_lo,
+                                          int row_hi, const gdmk::RkOut &rk, hipStream_t st) {
+  using namespace gdmk;
+  if (n_lines <= 0 || len <= 0) return hipSuccess;
+  auto al16 = [](const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (len % 2 != 0 || !al16(src) || !al16(rk.acc_in) || !al16(rk.acc_out) || (rk.Y && (!al16(rk.y) || !al16(rk.Y))))
+    return hipErrorNotSupported;
+  switch (p) {
+    case 3: return launch_mass3_rk_p<3>(src, len, n_lines, lrow, urow, invd, cst, row_lo, row_hi, rk, st);
+    case 5: return launch_mass3_rk_p<5>(src, len, n_lines, lrow, urow, invd, cst, row_lo, row_hi, rk, st);
+    case 7: return launch_mass3_rk_p<7>(src, len, n_lines, lrow, urow, invd, cst, row_lo, row_hi, rk, st);
+    default: return hipErrorNotSupported;
+  }
+}
 
 // v3 single-sweep line solves.  Tables: lrow [rows][p], urow [rows][p], invd
 // [rows], rows >= len + 3 C + p with zero rows from len on; cst = the interior

@@ -46,19 +46,21 @@ __global__ void __launch_bounds__(256) rk_update2_kernel(int64_t n, double beta,
   const int64_t n2 = n / 2, stride = (int64_t)gridDim.x * blockDim.x;
   const d2 *k2 = reinterpret_cast<const d2 *>(k), *a2 = reinterpret_cast<const d2 *>(acc_in);
   d2 *o2 = reinterpret_cast<d2 *>(acc_out);
+  const d2 av = {alpha, alpha}, bv = {beta, beta};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
     const d2 ki = __builtin_nontemporal_load(k2 + i);
     const d2 ai = __builtin_nontemporal_load(a2 + i);
+    // one FMA per update (the arithmetic of the x pass with the update fused, gdm_mass.hip)
     if (WITH_Y) {
       const d2 yi = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(y) + i);
-      __builtin_nontemporal_store(yi + alpha * ki, reinterpret_cast<d2 *>(Y) + i);
+      __builtin_nontemporal_store(__builtin_elementwise_fma(av, ki, yi), reinterpret_cast<d2 *>(Y) + i);
     }
-    __builtin_nontemporal_store(ai + beta * ki, o2 + i);
+    __builtin_nontemporal_store(__builtin_elementwise_fma(bv, ki, ai), o2 + i);
   }
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     const double ki = k[n - 1];
-    if (WITH_Y) Y[n - 1] = y[n - 1] + alpha * ki;
-    acc_out[n - 1] = acc_in[n - 1] + beta * ki;
+    if (WITH_Y) Y[n - 1] = fma(alpha, ki, y[n - 1]);
+    acc_out[n - 1] = fma(beta, ki, acc_in[n - 1]);
   }
 }
 
@@ -70,12 +72,12 @@ __global__ void __launch_bounds__(256) rk_update_kernel(int64_t n, double beta, 
   if (Y) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
       const double ki = k[i];
-      acc_out[i] = acc_in[i] + beta * ki;
-      Y[i] = y[i] + alpha * ki;
+      acc_out[i] = fma(beta, ki, acc_in[i]);
+      Y[i] = fma(alpha, ki, y[i]);
     }
   } else {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-      acc_out[i] = acc_in[i] + beta * k[i];
+      acc_out[i] = fma(beta, k[i], acc_in[i]);
   }
 }
 

@@ -130,6 +130,7 @@ def load():
         "gdm_apply_planes": [P, P, P, i32, i32],
         "gdm_mass_apply": [P, P, P],
         "gdm_mass_solve": [P, P, P],
+        "gdm_mass_solve_rk": [P, P, d, P, P, d, P, P],
         "gdm_constraints_distribute": [P, P],
         "gdm_mass_solve_cg": [P, P, P, d, d, i32, i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(d)],
         "gdm_mass_solve_lines": [P, i32, P, i64, i64, i64, i64, i64],

@@ -140,6 +140,20 @@ class GdmOperator:
         check(self.lib.gdm_mass_apply(self.h, _ptr(src_local), _ptr(dst_owned)), "gdm_mass_apply")
         return dst_owned
 
+    def mass_solve_rk(self, rhs_owned, beta, acc_in, acc_out, alpha=0.0, y=None, Y=None):
+        """k = M^-1 rhs; acc_out = acc_in + beta k; Y = y + alpha k (when Y is
+        given), with the update fused into the last line-solve pass
+        (gdm_mass_solve_rk): rhs_owned is overwritten; the same bits as
+        mass_solve(rhs, rhs) + rk_update"""
+        n = self.n_owned
+        for v in (rhs_owned, acc_in, acc_out) + ((y, Y) if Y is not None else ()):
+            if v.numel() != n:
+                raise GdmError("mass_solve_rk: vectors need n_owned = %d entries" % n)
+        check(self.lib.gdm_mass_solve_rk(self.h, _ptr(rhs_owned), float(beta), _ptr(acc_in), _ptr(acc_out),
+                                         float(alpha), _ptr(y) if Y is not None else None, _ptr(Y)),
+              "gdm_mass_solve_rk")
+        return acc_out
+
     def mass_solve(self, rhs_owned, x_owned):
         self._check_sizes(None, rhs_owned)
         self._check_sizes(None, x_owned)

@@ -86,17 +86,19 @@ class WaveProblem:
         stage = y
         for s in range(4):
             # k = (stage_v, M^-1 K stage_u)
-            self.rhs(t + RK4_C[s] * h, stage[0], kv)
+            op.apply(stage[0], kv)
             ku = stage[1]
             last = s == 3
             acc_in = y if s == 0 else acc
             acc_out = y if last else acc
             a_next = 0.0 if last else h * RK4_A[s]
-            # u block first: it reads ku = stage_v before the v block overwrites Y_v
+            # u block first (stage_u is consumed): it reads ku = stage_v before
+            # the v block overwrites Y_v
             op.rk_update(h * RK4_B[s], ku, acc_in[0], acc_out[0], a_next, None if last else y[0],
                          None if last else Y[0])
-            op.rk_update(h * RK4_B[s], kv, acc_in[1], acc_out[1], a_next, None if last else y[1],
-                         None if last else Y[1])
+            # v block: the mass solve with the update fused into its last pass
+            op.mass_solve_rk(kv, h * RK4_B[s], acc_in[1], acc_out[1], a_next, None if last else y[1],
+                             None if last else Y[1])
             stage = Y
 
     def run(self, start_t, end_t, dt, max_steps=None, callback=None):
@@ -153,10 +155,9 @@ class AdvectionProblem:
             for s in range(4):
                 alpha, t_k = (0.0, t) if s == 0 else (h * RK4_A[s - 1], t + RK4_C[s - 1] * h)
                 op.apply_bc_fn(stage, k, self.fn, self.prm, t, alpha, t_k)
-                op.mass_solve(k, k)
                 last = s == 3
-                op.rk_update(h * RK4_B[s], k, y if s == 0 else acc, y if last else acc,
-                             0.0 if last else h * RK4_A[s], None if last else y, None if last else Y)
+                op.mass_solve_rk(k, h * RK4_B[s], y if s == 0 else acc, y if last else acc,
+                                 0.0 if last else h * RK4_A[s], None if last else y, None if last else Y)
                 stage = Y
             return
         self.initialize_time_step(t)

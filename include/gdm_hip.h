@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 11
+#define GDM_HIP_ABI_VERSION 12
 
 enum gdm_status {
   GDM_OK = 0,
@@ -189,6 +189,14 @@ int gdm_mass_apply(gdm_op *op, const double *src_local, double *dst_owned);
 /* x_owned = M^-1 rhs_owned (exact Kronecker inverse; single rank; not with
  * periodic constraints: gdm_mass_solve_cg) */
 int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned);
+/* gdm_mass_solve_rk: k = M^-1 rhs, then gdm_vec_rk_update's acc_out = acc_in +
+ * beta k and, when Y != NULL, Y = y + alpha k -- one RK stage's solve and
+ * update (advection/problem.h:62-94 + the solve of :236-267) with the update
+ * fused into the last line-solve pass, so k never reaches HBM.  rhs_owned is
+ * overwritten (scratch); acc_in may equal acc_out.  Same bits as
+ * gdm_mass_solve(rhs, rhs) + gdm_vec_rk_update.  Single rank, non-periodic. */
+int gdm_mass_solve_rk(gdm_op *op, double *rhs_owned, double beta, const double *acc_in, double *acc_out,
+                      double alpha, const double *y, double *Y);
 
 /* Distributed exact mass inverse (n_ranks > 1; replaces the CG + ILU/AMG
  * solve of advection/problem.h:236-267 / wave/problem.h:457-502 across MPI

@@ -79,3 +79,74 @@ def test_apply_bc_fn_argument_errors():
     wave = gdm_amd.GdmOperator(2, 3, 6, -1.0, 1.0, "wave")
     with pytest.raises(gdm_amd.GdmError):
         wave.apply_bc_fn(wave.new_vector(local=True), wave.new_vector(local=False), 0, [1.0], 0.0)
+
+
+@pytest.mark.parametrize("dim,p,n", [(3, 5, 181), (3, 7, 183), (3, 3, 200), (2, 5, (300, 200)), (3, 5, 9)])
+@pytest.mark.parametrize("mode", ["Y", "noY", "alias"])
+def test_mass_solve_rk_bitwise_equals_separate(dim, p, n, mode):
+    """gdm_mass_solve_rk (the RK update fused into the x line-solve pass when
+    that pass runs unsegmented, 3D meshes with >= 32768 lines per pass; the
+    separate kernels otherwise) == gdm_mass_solve + gdm_vec_rk_update, bitwise"""
+    import gdm_amd
+
+    op = gdm_amd.GdmOperator(dim, p, n, 0.0, 1.0, "advection", params=(1.0, 0.15, -0.05)[:dim])
+    m = op.n_owned
+    g = torch.Generator(device="cuda").manual_seed(11)
+    r = lambda: torch.rand(m, dtype=torch.float64, device="cuda", generator=g) - 0.5  # noqa: E731
+    rhs, acc, y = r(), r(), r()
+    beta, alpha = 0.0123456789, -0.0234567891
+    # reference: separate solve + update
+    k = rhs.clone()
+    op.mass_solve(k, k)
+    acc_ref, Y_ref = acc.clone(), torch.empty_like(y)
+    if mode == "Y":
+        op.rk_update(beta, k, acc, acc_ref, alpha, y, Y_ref)
+    elif mode == "noY":
+        op.rk_update(beta, k, acc, acc_ref)
+    else:
+        op.rk_update(beta, k, acc_ref, acc_ref, alpha, y, Y_ref)
+    acc_out, Y = acc.clone(), torch.empty_like(y)
+    rhs2 = rhs.clone()
+    if mode == "Y":
+        op.mass_solve_rk(rhs2, beta, acc, acc_out, alpha, y, Y)
+    elif mode == "noY":
+        op.mass_solve_rk(rhs2, beta, acc, acc_out)
+    else:
+        op.mass_solve_rk(rhs2, beta, acc_out, acc_out, alpha, y, Y)
+    torch.cuda.synchronize()
+    assert torch.equal(acc_out, acc_ref), float((acc_out - acc_ref).abs().max())
+    if mode != "noY":
+        assert torch.equal(Y, Y_ref), float((Y - Y_ref).abs().max())
+
+
+@pytest.mark.parametrize("dim,p,n", [(3, 5, 181), (2, 5, (13, 10))])
+def test_wave_problem_fused_step_vs_oracle_form(dim, p, n):
+    """WaveProblem (v block through gdm_mass_solve_rk) == the same stages with
+    mass_solve + rk_update, bitwise"""
+    import gdm_amd
+    from gdm_amd.problem import RK4_A, RK4_B
+
+    op = gdm_amd.GdmOperator(dim, p, n, -1.21, 1.21, "wave")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    u0 = torch.rand(op.n_owned, dtype=torch.float64, device="cuda", generator=g)
+    pr = gdm_amd.WaveProblem(op)
+    pr.u.copy_(u0)
+    h = 1e-3
+    pr.step(0.0, h)
+    # unfused restatement of one step
+    y = (u0.clone(), torch.zeros_like(u0))
+    acc = [torch.empty_like(u0) for _ in range(2)]
+    Y = [torch.empty_like(u0) for _ in range(2)]
+    kv = torch.empty_like(u0)
+    stage = y
+    for s in range(4):
+        op.apply(stage[0], kv)
+        op.mass_solve(kv, kv)
+        last = s == 3
+        ai, ao = (y if s == 0 else acc), (y if last else acc)
+        a_next = 0.0 if last else h * RK4_A[s]
+        op.rk_update(h * RK4_B[s], stage[1], ai[0], ao[0], a_next, None if last else y[0], None if last else Y[0])
+        op.rk_update(h * RK4_B[s], kv, ai[1], ao[1], a_next, None if last else y[1], None if last else Y[1])
+        stage = Y
+    torch.cuda.synchronize()
+    assert torch.equal(pr.u, y[0]) and torch.equal(pr.v, y[1])
