@@ -53,26 +53,50 @@ __device__ __forceinline__ double bc_point(const BcGeom &g, const BcFace &F, con
     for (int d = 0; d < g.dim; ++d) r2 += (x[d] - f.prm[1 + d]) * (x[d] - f.prm[1 + d]);
     return fmax(0.0, f.prm[0] - sqrt(r2));
   }
-  // kind 2: prod_d sin(.) over the dim directions; trivial slots hold (1, 0)
+  return 0.0;  // kind 2: bc_sine_point
+}
+
+// GDM_FN_SINE_PRODUCT at point (i0, i1) of a face from its factor table at the
+// same time: prod_d sin(.) (trivial slots hold (1, 0)); d/dt = sum over the
+// directions of P_e cos(.) * the other sines, added without contraction so the
+// stored and the in-kernel evaluations round alike
+__device__ __forceinline__ double bc_sine_point(const double *__restrict__ tab, int ld, const BcSine &w, int i0,
+                                                int i1, int derivative) {
   const double s0 = tab[2 * i0], c0 = tab[2 * i0 + 1];
   const double s1 = tab[2 * ((size_t)ld + i1)], c1 = tab[2 * ((size_t)ld + i1) + 1];
   const double sn = tab[2 * (size_t)2 * ld], cn = tab[2 * (size_t)2 * ld + 1];
   if (!derivative) return s0 * s1 * sn;
-  // d/dt: sum over directions of -2 pi k_e a_e cos(.) * the other sines
   double r = 0.0;
-  if (F.dim_index[0] >= 0) r += -2.0 * M_PI * f.prm[3 + F.dim_index[0]] * f.prm[F.dim_index[0]] * c0 * s1 * sn;
-  if (F.dim_index[1] >= 0) r += -2.0 * M_PI * f.prm[3 + F.dim_index[1]] * f.prm[F.dim_index[1]] * s0 * c1 * sn;
-  r += -2.0 * M_PI * f.prm[3 + F.d] * f.prm[F.d] * s0 * s1 * cn;
+  {
+#pragma clang fp contract(off)
+    if (w.has0) r = r + w.P0 * c0 * s1 * sn;
+    if (w.has1) r = r + w.P1 * s0 * c1 * sn;
+    r = r + w.Pn * s0 * s1 * cn;
+  }
+  asm volatile("" : "+v"(r));
   return r;
+}
+
+// the compact stage value (kinds 2 and 0): y + alpha k with y = g(t_g), k =
+// dg/dt(t_k), as rk_update2_kernel forms Y (GDM_FN_CONSTANT: dg/dt = 0)
+__device__ __forceinline__ double bc_stage_face_value(const BcStageFace &s, int i0, int i1) {
+  if (s.kind == 0) return s.c;
+  const double y = bc_sine_point(s.tg, s.ld, s.w, i0, i1, 0);
+  if (s.alpha == 0.0) return y;
+  return fma(s.alpha, bc_sine_point(s.tk, s.ld, s.w, i0, i1, 1), y);
 }
 
 // the stage boundary value Y = y + alpha k of the RK stages with y = g(t_g)
 // and k = dg/dt(t_k) (alpha = 0: y), written as rk_update2_kernel writes Y
+// (generic form, any kind; the face kernels use it for GDM_FN_CONE)
 __device__ __forceinline__ double bc_stage_value(const BcStage &s, int i0, int i1) {
   const BcFace &F = s.g.face[s.face];
-  const double y = bc_point(s.g, F, s.f, s.tab + (size_t)s.face * 3 * s.ld * 2, s.ld, i0, i1, 0);
+  const double *tg = s.tab + (size_t)s.face * 3 * s.ld * 2;
+  const double *tk = s.tab + (size_t)(BcStage::kMaxFaces + s.face) * 3 * s.ld * 2;
+  const BcSine w = bc_sine_weights(s.f, F);
+  const double y = s.f.kind == 2 ? bc_sine_point(tg, s.ld, w, i0, i1, 0) : bc_point(s.g, F, s.f, tg, s.ld, i0, i1, 0);
   if (s.alpha == 0.0) return y;
-  const double k = bc_point(s.g, F, s.f, s.tab + (size_t)(BcStage::kMaxFaces + s.face) * 3 * s.ld * 2, s.ld, i0, i1, 1);
+  const double k = s.f.kind == 2 ? bc_sine_point(tk, s.ld, w, i0, i1, 1) : bc_point(s.g, F, s.f, tk, s.ld, i0, i1, 1);
   return fma(s.alpha, k, y);
 }
 

@@ -155,6 +155,7 @@ struct gdm_op {
   static constexpr int n_err_partial = 1024;
   int bc_tab_ld = 0;
   double *bc_stage_tab = nullptr;  // gdm_apply_bc_fn: BcStage factor tables (2 x 6 faces)
+  double *bc_stage_vals = nullptr;  // gdm_apply_bc_fn: the stage boundary values (n_bc_points)
   int bc_stage_ld = 0;
   // periodicity constraints (system.h:427-463): scratch copy of the input for
   // distribute; CG work vectors and the Jacobi inverse diagonal
@@ -800,20 +801,18 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
 // stage (non-NULL): the boundary values are evaluated from its function
 // (gdm_apply_bc_fn) instead of read from bc_values
 void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
-                          hipStream_t st = nullptr, const gdmk::BcStage *stage = nullptr) {
+                          hipStream_t st = nullptr) {
   if (op->kind != GDM_OP_ADVECTION) return;
+  constexpr int kMax = gdmk::BcStage::kMaxFaces;
+  if (op->faces.size() > (size_t)kMax) throw std::runtime_error("more than 6 boundary faces");
+  gdmk::FaceArgs fas[kMax] = {};
+  int nf = 0;
+  bool all_g = true;
   for (size_t fi = 0; fi < op->faces.size(); ++fi) {
     const Face &F = op->faces[fi];
     if (F.scale == 0.0) continue;
-    gdmk::FaceArgs fa{};
-    gdmk::BcStage fs{};
-    if (stage) {
-      fs = *stage;
-      fs.face = (int)fi;
-      fa.stage = &fs;
-    } else {
-      fa.U = bc_values + F.offset;
-    }
+    gdmk::FaceArgs &fa = fas[nf];
+    fa.U = bc_values + F.offset;
     fa.Q0 = F.t0.Q;
     fa.Q1 = F.t1.Q;
     fa.i0_begin = F.t0.node_begin;
@@ -842,15 +841,26 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     fa.stride1 = F.t1.stride;
     fa.scale = F.scale;
     fa.phase = phase;
-    // one face after the other: two faces share the box-edge nodes, and a
-    // concurrent step 2 (one launch, fp64 atomics on the edges) made the
-    // edge sums order-dependent, which the bit-exact rank / communicator
-    // comparisons of tests/test_host_mpi.py catch.  Phase 3 (side stream)
-    // computes every face's step 2 into its own buffer G while the stencil
-    // runs; phase 4 adds the buffers into dst face by face in the same order
-    // (the same roundings as phase 0's dst += scale s)
-    if (phase == 3 && !F.G) fa.phase = 1;  // (no buffer: cannot happen for inflow faces)
-    hip_check(gdmk_launch_face(fa, (phase == 1 || phase == 3) && st ? st : op->stream), "face launch");
+    all_g = all_g && F.G && F.T;
+    ++nf;
+  }
+  // Phase 3 (side stream): every face's step 1 and its step 2 into its own
+  // buffer G while the stencil runs, all faces in one launch per step (each
+  // face has its own T and G); phase 4 adds the buffers into dst face by face
+  // in face order (the same roundings as phase 0's dst += scale s).  Phases
+  // 0 / 4 run one face after the other: two faces share the box-edge nodes,
+  // and a concurrent add (fp64 atomics on the edges) made the edge sums
+  // order-dependent, which the bit-exact rank / communicator comparisons of
+  // tests/test_host_mpi.py catch.
+  const hipStream_t fst = (phase == 1 || phase == 3) && st ? st : op->stream;
+  if (phase == 3 && all_g) {
+    const hipError_t e = gdmk_launch_faces_g(fas, nf, fst);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotSupported) hip_check(e, "faces launch");
+  }
+  for (int i = 0; i < nf; ++i) {
+    if (phase == 3 && !fas[i].G) fas[i].phase = 1;  // (no buffer: cannot happen for inflow faces)
+    hip_check(gdmk_launch_face(fas[i], fst), "face launch");
   }
 }
 
@@ -1813,14 +1823,16 @@ int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_param
   GDM_GUARD_END
 }
 
-int gdm_apply_bc_fn(gdm_op *op, const double *src_local, double *dst_owned, int fn_kind, const double *params,
-                    int n_params, double t_g, double alpha, double t_k) {
-  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
-  if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
-  if (op->kind != GDM_OP_ADVECTION) return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_bc_fn: advection operators only");
-  if (int rc = check_bc_fn(op, fn_kind, params, n_params)) return rc;
-  GDM_GUARD_BEGIN
-  hip_check(hipSetDevice(op->device), "hipSetDevice");
+}  // extern "C"
+
+namespace {
+
+// the stage boundary values g(t_g) + alpha dg/dt(t_k) of a built-in function
+// into the operator's block(0)-sized scratch (tables + one fill launch on
+// `st`); returns the scratch (NULL without boundary points)
+const double *fill_stage_boundary(gdm_op *op, int fn_kind, const double *params, int n_params, double t_g,
+                                  double alpha, double t_k, hipStream_t st) {
+  if (op->layout.n_bc_points <= 0) return nullptr;
   gdmk::BcStage stage{};
   int ld = 1;
   build_bc_fn(op, fn_kind, params, n_params, stage.g, stage.f, ld);
@@ -1829,30 +1841,50 @@ int gdm_apply_bc_fn(gdm_op *op, const double *src_local, double *dst_owned, int 
     op->bc_stage_tab = keep(op, dev_upload(zero));
     op->bc_stage_ld = ld;
   }
+  if (!op->bc_stage_vals) {
+    hip_check(hipMalloc(&op->bc_stage_vals, sizeof(double) * op->layout.n_bc_points), "hipMalloc");
+    keep(op, op->bc_stage_vals);
+  }
   stage.tab = op->bc_stage_tab;
   stage.ld = op->bc_stage_ld;
   stage.alpha = alpha;
-  const bool bc = op->layout.n_bc_points > 0;
-  const int with_k = alpha != 0.0 ? 1 : 0;
+  hip_check(gdmk_launch_bc_tables(stage.g, stage.f, t_g, t_k, alpha != 0.0 ? 1 : 0, op->bc_stage_tab, stage.ld, st),
+            "bc tables");
+  // only the inflow faces: the others' values are never read (scale 0)
+  int faces[gdmk::BcStage::kMaxFaces], n = 0;
+  for (size_t fi = 0; fi < op->faces.size(); ++fi)
+    if (op->faces[fi].scale != 0.0) faces[n++] = (int)fi;
+  hip_check(gdmk_launch_bc_stage_fill(stage, faces, n, op->bc_stage_vals, st), "bc stage fill");
+  return op->bc_stage_vals;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gdm_apply_bc_fn(gdm_op *op, const double *src_local, double *dst_owned, int fn_kind, const double *params,
+                    int n_params, double t_g, double alpha, double t_k) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
+  if (op->kind != GDM_OP_ADVECTION) return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_bc_fn: advection operators only");
+  if (int rc = check_bc_fn(op, fn_kind, params, n_params)) return rc;
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  // the stage values first, on the op stream (~28 M points at C3: one write
+  // pass), then gdm_apply with them; a side-stream launch would wait for the
+  // interior launch's workgroups (one per CU, all of its LDS) to drain
+  const double *bc = fill_stage_boundary(op, fn_kind, params, n_params, t_g, alpha, t_k, op->stream);
   if (op->concurrent && !op->mesh.periodic) {
-    // as gdm_apply: the factor tables, the z-wall launch and the faces' step 1
-    // + 2 (into G) on the side stream, dst += G after the join
     hip_check(hipEventRecord(op->ev_fork, op->stream), "hipEventRecord");
     hip_check(hipStreamWaitEvent(op->side_stream, op->ev_fork, 0), "hipStreamWaitEvent");
-    if (bc)
-      hip_check(gdmk_launch_bc_tables(stage.g, stage.f, t_g, t_k, with_k, op->bc_stage_tab, stage.ld, op->side_stream),
-                "bc tables");
     hip_check(launch_stencil(op, false, src_local, dst_owned, -1, -1, op->side_stream), "stencil launch");
-    if (bc) launch_boundary_data(op, nullptr, dst_owned, 3, op->side_stream, &stage);
+    if (bc) launch_boundary_data(op, bc, dst_owned, 3, op->side_stream);
     hip_check(hipEventRecord(op->ev_join, op->side_stream), "hipEventRecord");
     hip_check(hipStreamWaitEvent(op->stream, op->ev_join, 0), "hipStreamWaitEvent");
-    if (bc) launch_boundary_data(op, nullptr, dst_owned, 4);
+    if (bc) launch_boundary_data(op, bc, dst_owned, 4);
   } else {
-    if (bc)
-      hip_check(gdmk_launch_bc_tables(stage.g, stage.f, t_g, t_k, with_k, op->bc_stage_tab, stage.ld, op->stream),
-                "bc tables");
     any_stencil(op, false, src_local, dst_owned);
-    if (bc) launch_boundary_data(op, nullptr, dst_owned, 0, nullptr, &stage);
+    if (bc) launch_boundary_data(op, bc, dst_owned);
   }
   return GDM_OK;
   GDM_GUARD_END
@@ -1867,21 +1899,8 @@ int gdm_add_boundary_fn(gdm_op *op, double *dst_owned, int fn_kind, const double
   if (op->layout.n_bc_points == 0) return GDM_OK;
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
-  gdmk::BcStage stage{};
-  int ld = 1;
-  build_bc_fn(op, fn_kind, params, n_params, stage.g, stage.f, ld);
-  if (!op->bc_stage_tab || op->bc_stage_ld < ld) {
-    std::vector<double> zero((size_t)2 * gdmk::BcStage::kMaxFaces * 3 * ld * 2, 0.0);
-    op->bc_stage_tab = keep(op, dev_upload(zero));
-    op->bc_stage_ld = ld;
-  }
-  stage.tab = op->bc_stage_tab;
-  stage.ld = op->bc_stage_ld;
-  stage.alpha = alpha;
-  hip_check(gdmk_launch_bc_tables(stage.g, stage.f, t_g, t_k, alpha != 0.0 ? 1 : 0, op->bc_stage_tab, stage.ld,
-                                  op->stream),
-            "bc tables");
-  launch_boundary_data(op, nullptr, dst_owned, 0, nullptr, &stage);
+  const double *bc = fill_stage_boundary(op, fn_kind, params, n_params, t_g, alpha, t_k, op->stream);
+  launch_boundary_data(op, bc, dst_owned);
   return GDM_OK;
   GDM_GUARD_END
 }

@@ -63,7 +63,6 @@ struct StencilArgs {
 // t0, t1; trivial directions have one node, one point and weight 1).
 struct FaceArgs {
   const double *U;  // [Q1][Q0] stage boundary values of the face
-  const BcStage *stage;  // or (non-NULL) evaluated from a built-in function (gdm_apply_bc_fn)
   int Q0, Q1;
   int i0_begin, i0_end, i1_begin, i1_end;  // owned output nodes
   const int *qs0, *qs1, *qc1;
@@ -146,6 +145,10 @@ hipError_t gdmk_launch_mass3_rk(int p, const double *src, int len, int64_t n_lin
                                 const double *urow, const double *invd, const double *cst, int row_lo, int row_hi,
                                 const gdmk::RkOut &rk, hipStream_t st);
 hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st);
+// phase 3 of n inflow faces (step 1 + step 2 into each face's own G) in two
+// launches; hipErrorNotSupported unless every face uses the cell form of step 1
+// with its own T and G (the caller then launches face by face)
+hipError_t gdmk_launch_faces_g(const gdmk::FaceArgs *fa, int n, hipStream_t st);
 hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st);
 hipError_t gdmk_launch_dot(int64_t n, const double *x, const double *y, double *partial, int n_partial, double *out,
                            hipStream_t st);

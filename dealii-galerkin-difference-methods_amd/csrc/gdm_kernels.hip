@@ -22,7 +22,6 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "gdm_bcfn.h"
 #include "gdm_coeffs.h"
 #include "gdm_kernels.h"
 
@@ -1731,17 +1730,16 @@ __global__ void __launch_bounds__(256) chol_lines_kernel(double *__restrict__ v,
 // in LDS with coalesced loads; each lane then owns one node and reads its
 // weights node-minor (w0T), so every global access is a contiguous wave row.
 // ---------------------------------------------------------------------------
-// boundary values U(i0, i1) of the face: stored ([Q1][Q0] array, gdm_apply)
-// or evaluated from a built-in function at the stage time (gdm_apply_bc_fn)
+// boundary values U(i0, i1) of the face ([Q1][Q0] array).  (Evaluating the
+// stage values of a built-in function here instead, per point, measured 2-3x
+// slower than reading them: each lane's six consecutive points make every
+// table read touch 64 cache lines; gdm_apply_bc_fn fills the array first.)
 struct BcArr {
   const double *__restrict__ U;
   int Q0;
   __device__ __forceinline__ double operator()(int i0, int i1) const { return U[(int64_t)i1 * Q0 + i0]; }
 };
-struct BcFnSrc {
-  BcStage s;
-  __device__ __forceinline__ double operator()(int i0, int i1) const { return bc_stage_value(s, i0, i1); }
-};
+
 
 template <int ROWS, class Src>
 __global__ void __launch_bounds__(FACE_CHUNK) face_step1_kernel(const Src U, int Q0, int Q1,
@@ -1795,16 +1793,16 @@ __device__ __forceinline__ int face_box_offset(int c, int p, int n) {
 }
 
 template <int P, class Src>
-__global__ void __launch_bounds__(512) face_cell_step1_kernel(const Src U, int Q0, int Q1, int rpb,
-                                                               int i0_begin, int n0, const int *__restrict__ crange,
-                                                               const double *__restrict__ phi, int ncell_total,
-                                                               int cell_begin, double *__restrict__ T) {
+__device__ __forceinline__ void face_cell_step1_body(const Src &U, int Q0, int Q1, int rpb, int i0_begin, int n0,
+                                                     const int *__restrict__ crange, const double *__restrict__ phi,
+                                                     int ncell_total, int cell_begin, double *__restrict__ T,
+                                                     int block) {
   constexpr int N1 = P + 1;
   extern __shared__ double sh[];  // [P][N1][N1] Phi, then [ncells][N1] S
   double *sphi = sh, *S = sh + P * N1 * N1;
   const int ncells = Q0 / N1;
   for (int e = threadIdx.x; e < P * N1 * N1; e += blockDim.x) sphi[e] = phi[e];
-  const int r0 = blockIdx.x * rpb, r1 = min(Q1, r0 + rpb);
+  const int r0 = block * rpb, r1 = min(Q1, r0 + rpb);
   for (int row = r0; row < r1; ++row) {
     __syncthreads();  // Phi ready / previous row's gather done
     for (int c = threadIdx.x; c < ncells; c += blockDim.x) {
@@ -1832,10 +1830,62 @@ __global__ void __launch_bounds__(512) face_cell_step1_kernel(const Src U, int Q
   }
 }
 
+template <int P, class Src>
+__global__ void __launch_bounds__(512) face_cell_step1_kernel(const Src U, int Q0, int Q1, int rpb,
+                                                               int i0_begin, int n0, const int *__restrict__ crange,
+                                                               const double *__restrict__ phi, int ncell_total,
+                                                               int cell_begin, double *__restrict__ T) {
+  face_cell_step1_body<P>(U, Q0, Q1, rpb, i0_begin, n0, crange, phi, ncell_total, cell_begin, T, blockIdx.x);
+}
+
+// every inflow face's step 1 (cell form) in one launch, face = blockIdx.y:
+// the faces are independent (own T), so their rows share the GPU instead of
+// running one face after the other (gdmk_launch_faces_g)
+template <class Src>
+struct Step1Face {
+  Src U;
+  int Q0, Q1, i0_begin, n0;
+  const int *crange;
+  const double *phi;
+  int ncell_total, cell_begin;
+  double *T;
+};
+template <class Src>
+struct Step1Set {
+  Step1Face<Src> f[BcStage::kMaxFaces];
+  int rpb;
+};
+template <int P, class Src>
+__global__ void __launch_bounds__(512) face_cell_step1_multi_kernel(const Step1Set<Src> set) {
+  const Step1Face<Src> &F = set.f[blockIdx.y];
+  if ((int)blockIdx.x * set.rpb >= F.Q1) return;
+  face_cell_step1_body<P>(F.U, F.Q0, F.Q1, set.rpb, F.i0_begin, F.n0, F.crange, F.phi, F.ncell_total, F.cell_begin,
+                          F.T, blockIdx.x);
+}
+
 // dst node (t, i1) += scale sum_m w1[i1][m] T[q + m][t].  The product is
 // rounded before the add (no FMA contraction into it), so the result equals
 // G = scale s then dst + G (ASSIGN: G written node-major, added by
 // face_add_kernel after the stencil): the same bits on both paths.
+// scale sum_m w1[i1][m] T[q + m][t], the product rounded on its own: the
+// compiler may not fuse it into a later add (one FMA would round differently
+// from G + dst)
+__device__ __forceinline__ double face_step2_value(const double *__restrict__ T, int n0, int t, int i1,
+                                                   const int *__restrict__ qs1, const int *__restrict__ qc1,
+                                                   const double *__restrict__ w1, int wmax1, double scale) {
+  const double *w = w1 + (int64_t)i1 * wmax1;
+  const int n = qc1[i1], q = qs1[i1];
+  double s = 0.0;
+  for (int m = 0; m < n; ++m) s = fma(w[m], T[(int64_t)(q + m) * n0 + t], s);
+  double v;
+  {
+#pragma clang fp contract(off)
+    v = scale * s;
+  }
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 template <bool ASSIGN>
 __global__ void __launch_bounds__(256) face_step2_kernel(const double *__restrict__ T, int n0, int i1_begin,
                                                           int i1_end, const int *__restrict__ qs1,
@@ -1846,24 +1896,34 @@ __global__ void __launch_bounds__(256) face_step2_kernel(const double *__restric
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int i1 = i1_begin + (int)blockIdx.y;
   if (t >= n0 || i1 >= i1_end) return;
-  const double *w = w1 + (int64_t)i1 * wmax1;
-  const int n = qc1[i1], q = qs1[i1];
-  double s = 0.0;
-  for (int m = 0; m < n; ++m) s = fma(w[m], T[(int64_t)(q + m) * n0 + t], s);
-  // the product is rounded on its own: the compiler may not fuse it into the
-  // add below (one FMA would round differently from G + dst)
-  double v;
-  {
-#pragma clang fp contract(off)
-    v = scale * s;
-  }
-  asm volatile("" : "+v"(v));
+  const double v = face_step2_value(T, n0, t, i1, qs1, qc1, w1, wmax1, scale);
   if constexpr (ASSIGN) {
     dst[(int64_t)(i1 - i1_begin) * n0 + t] = v;
   } else {
     double *d = dst + base + (int64_t)t * stride0 + (int64_t)(i1 - i1_begin) * stride1;
     *d = *d + v;
   }
+}
+
+// every inflow face's step 2 into its G in one launch, face = blockIdx.z
+struct Step2Face {
+  const double *T;
+  int n0, i1_begin, i1_end;
+  const int *qs1, *qc1;
+  const double *w1;
+  int wmax1;
+  double *G;
+  double scale;
+};
+struct Step2Set {
+  Step2Face f[BcStage::kMaxFaces];
+};
+__global__ void __launch_bounds__(256) face_step2_multi_kernel(const Step2Set set) {
+  const Step2Face &F = set.f[blockIdx.z];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i1 = F.i1_begin + (int)blockIdx.y;
+  if (t >= F.n0 || i1 >= F.i1_end) return;
+  F.G[(int64_t)(i1 - F.i1_begin) * F.n0 + t] = face_step2_value(F.T, F.n0, t, i1, F.qs1, F.qc1, F.w1, F.wmax1, F.scale);
 }
 
 // dst node (t, i1) += G[i1][t]: one launch per face, in face order
@@ -2197,13 +2257,57 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
       hipLaunchKernelGGL(face_step2_kernel<false>, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1,
                          f.w1, f.wmax1, f.dst, f.base, f.stride0, f.stride1, f.scale);
   };
-  if (f.stage) {
-    BcFnSrc s{*f.stage};
-    return face_launch(f, s, st, step2);
-  }
   return face_launch(f, BcArr{f.U, f.Q0}, st, step2);
 }
 
+
+template <class Src, class Get>
+static hipError_t faces_g_launch(const gdmk::FaceArgs *fa, int n, Get &&src, hipStream_t st) {
+  using namespace gdmk;
+  Step1Set<Src> s1{};
+  Step2Set s2{};
+  s1.rpb = 4;
+  size_t lds = 0;
+  int g1 = 0, g2x = 0, g2y = 0;
+  for (int i = 0; i < n; ++i) {
+    const FaceArgs &f = fa[i];
+    const int n0 = f.i0_end - f.i0_begin;
+    s1.f[i] = Step1Face<Src>{src(f), f.Q0, f.Q1, f.i0_begin, n0, f.crange0, f.phi0, f.ncell0_total, f.cell0_begin,
+                             f.T};
+    s2.f[i] = Step2Face{f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1, f.G, f.scale};
+    lds = std::max(lds, sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)f.Q0));
+    g1 = std::max(g1, (f.Q1 + s1.rpb - 1) / s1.rpb);
+    g2x = std::max(g2x, (n0 + 255) / 256);
+    g2y = std::max(g2y, f.i1_end - f.i1_begin);
+  }
+  switch (fa[0].p) {
+#define GDM_FACES_G(PP)                                                                                   \
+  case PP:                                                                                              \
+    hipLaunchKernelGGL((face_cell_step1_multi_kernel<PP, Src>), dim3(g1, n), dim3(512), lds, st, s1); \
+    break;
+    GDM_FACES_G(1) GDM_FACES_G(3) GDM_FACES_G(5) GDM_FACES_G(7) GDM_FACES_G(9)
+#undef GDM_FACES_G
+    default: return hipErrorNotSupported;
+  }
+  hipLaunchKernelGGL(face_step2_multi_kernel, dim3(g2x, g2y, n), dim3(256), 0, st, s2);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gdmk_launch_faces_g(const gdmk::FaceArgs *fa, int n, hipStream_t st) {
+  using namespace gdmk;
+  if (n <= 0) return hipSuccess;
+  if (n > BcStage::kMaxFaces) return hipErrorNotSupported;
+  for (int i = 0; i < n; ++i) {
+    const FaceArgs &f = fa[i];
+    const size_t cell_lds = sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)f.Q0);
+    if (!f.phi0 || cell_lds > 48 * 1024 || !f.G || !f.T || f.p != fa[0].p || f.Q1 <= 0 ||
+        f.i0_end <= f.i0_begin || f.i1_end <= f.i1_begin)
+      return hipErrorNotSupported;
+    for (int j = 0; j < i; ++j)
+      if (fa[j].T == f.T || fa[j].G == f.G) return hipErrorNotSupported;  // faces must not share buffers
+  }
+  return faces_g_launch<BcArr>(fa, n, [](const FaceArgs &f) { return BcArr{f.U, f.Q0}; }, st);
+}
 
 extern "C" hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st) {
   using namespace gdmk;

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cmath>
+
 namespace gdmk {
 
 // Boundary-point geometry for device evaluation of boundary functions
@@ -28,6 +30,31 @@ struct BcGeom {
 struct BcFn {
   int kind, dim;
   double prm[12];
+};
+// GDM_FN_SINE_PRODUCT's d/dt weights of one face: P = -2 pi k_e a_e of its t0,
+// t1 and normal directions (has0 / has1: t0 / t1 non-trivial); the same host
+// arithmetic feeds the stored (bc_face_kernel) and the in-kernel evaluation
+struct BcSine {
+  double P0, P1, Pn;
+  int has0, has1;
+};
+__host__ __device__ inline BcSine bc_sine_weights(const BcFn &f, const BcFace &F) {
+  auto P = [&](int e) { return -2.0 * M_PI * f.prm[3 + e] * f.prm[e]; };
+  BcSine w{};
+  w.has0 = F.dim_index[0] >= 0;
+  w.has1 = F.dim_index[1] >= 0;
+  w.P0 = w.has0 ? P(F.dim_index[0]) : 0.0;
+  w.P1 = w.has1 ? P(F.dim_index[1]) : 0.0;
+  w.Pn = P(F.d);
+  return w;
+}
+// the compact stage source of one face for GDM_FN_SINE_PRODUCT / GDM_FN_CONSTANT
+// (no geometry: the per-point work is four table reads and a few multiplies)
+struct BcStageFace {
+  const double *tg, *tk;  // the face's [3][ld][2] factor tables at t_g, t_k
+  int ld, kind;
+  BcSine w;
+  double alpha, c;  // c: GDM_FN_CONSTANT's value
 };
 // the RK stage boundary values of one face, evaluated where they are read
 // (gdm_apply_bc_fn): y + alpha k with y = g(t_g), k = dg/dt(t_k); tab =
@@ -65,6 +92,9 @@ hipError_t gdmk_launch_vmul(int64_t n, const double *w, const double *x, double 
 // tab: scratch of n_faces * 3 * ld * 2 doubles, ld >= max(Q0, Q1)
 hipError_t gdmk_launch_bc_eval(const gdmk::BcGeom &g, const gdmk::BcFn &f, double t, int derivative, double *out,
                                double *tab, int ld, hipStream_t st);
+// the stage boundary values of BcStage into out (device block(0) order) for
+// the n faces faces[0..n): out = g(t_g) + alpha dg/dt(t_k), tables ready
+hipError_t gdmk_launch_bc_stage_fill(const gdmk::BcStage &s, const int *faces, int n, double *out, hipStream_t st);
 // the factor tables of BcStage (kind 2; nothing to do otherwise): every face
 // at t_g and, with_k, at t_k, one launch; tab holds 2 * 6 * 3 * ld * 2 doubles
 hipError_t gdmk_launch_bc_tables(const gdmk::BcGeom &g, const gdmk::BcFn &f, double t_g, double t_k, int with_k,

@@ -114,12 +114,14 @@ __global__ void __launch_bounds__(256) bc_tables_kernel(BcGeom g, BcFn f, double
 }
 
 // one face: grid (ceil(Q0 / 256), Q1); i1 = blockIdx.y, i0 = lane index
-__global__ void __launch_bounds__(256) bc_face_kernel(BcGeom g, BcFace F, BcFn f, double t, int derivative,
-                                                      const double *__restrict__ tab, int ld, double *out) {
+__global__ void __launch_bounds__(256) bc_face_kernel(BcGeom g, BcFace F, BcFn f, BcSine w, double t,
+                                                      int derivative, const double *__restrict__ tab, int ld,
+                                                      double *out) {
   const int i1 = blockIdx.y;
   const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (i0 >= F.Q[0]) return;
-  out[F.offset + (int64_t)i1 * F.Q[0] + i0] = bc_point(g, F, f, tab, ld, i0, i1, derivative);
+  out[F.offset + (int64_t)i1 * F.Q[0] + i0] =
+      f.kind == 2 ? bc_sine_point(tab, ld, w, i0, i1, derivative) : bc_point(g, F, f, tab, ld, i0, i1, derivative);
 }
 
 // Periodicity constraints of System::make_periodicity_constraints
@@ -304,8 +306,74 @@ extern "C" hipError_t gdmk_launch_bc_eval(const gdmk::BcGeom &g, const gdmk::BcF
                          tab + (size_t)fi * 3 * ld * 2, ld);
     }
     hipLaunchKernelGGL(gdmk::bc_face_kernel, dim3((unsigned)((F.Q[0] + 255) / 256), (unsigned)F.Q[1]), dim3(256), 0,
-                       st, g, F, f, t, derivative, tab + (size_t)fi * 3 * ld * 2, ld, out);
+                       st, g, F, f, gdmk::bc_sine_weights(f, F), t, derivative, tab + (size_t)fi * 3 * ld * 2, ld, out);
   }
+  return hipGetLastError();
+}
+
+namespace gdmk {
+// the faces to fill (kinds 2 and 0), compact per-face sources resolved on the
+// host: the kernel reads them from the argument block by blockIdx.z (scalar
+// loads, no private copy)
+struct BcFillSet {
+  BcStageFace fc[BcStage::kMaxFaces];
+  int64_t offset[BcStage::kMaxFaces];
+  int Q0[BcStage::kMaxFaces], Q1[BcStage::kMaxFaces];
+};
+// one face per blockIdx.z, lane = t0 point (coalesced table reads and writes)
+__global__ void __launch_bounds__(256) bc_stage_fill_kernel(const BcFillSet set, double *out) {
+  const int f = blockIdx.z, i1 = blockIdx.y, i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int q0 = set.Q0[f];
+  if (i0 >= q0 || i1 >= set.Q1[f]) return;
+  out[set.offset[f] + (int64_t)i1 * q0 + i0] = bc_stage_face_value(set.fc[f], i0, i1);
+}
+// GDM_FN_CONE (any geometry; small meshes): the generic evaluation, one face
+__global__ void __launch_bounds__(256) bc_stage_fill_generic_kernel(BcStage s, double *out) {
+  const BcFace &F = s.g.face[s.face];
+  const int i1 = blockIdx.y, i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 >= F.Q[0]) return;
+  out[F.offset + (int64_t)i1 * F.Q[0] + i0] = bc_stage_value(s, i0, i1);
+}
+}  // namespace gdmk
+
+extern "C" hipError_t gdmk_launch_bc_stage_fill(const gdmk::BcStage &s, const int *faces, int n, double *out,
+                                               hipStream_t st) {
+  using namespace gdmk;
+  if (n <= 0) return hipSuccess;
+  if (n > BcStage::kMaxFaces) return hipErrorInvalidValue;
+  if (s.f.kind == 1) {
+    for (int i = 0; i < n; ++i) {
+      BcStage one = s;
+      one.face = faces[i];
+      const BcFace &F = s.g.face[faces[i]];
+      if ((int64_t)F.Q[0] * F.Q[1] <= 0) continue;
+      hipLaunchKernelGGL(bc_stage_fill_generic_kernel, dim3((unsigned)((F.Q[0] + 255) / 256), (unsigned)F.Q[1]),
+                         dim3(256), 0, st, one, out);
+    }
+    return hipGetLastError();
+  }
+  BcFillSet set{};
+  int q0 = 0, q1 = 0;
+  for (int i = 0; i < n; ++i) {
+    const int fi = faces[i];
+    const BcFace &F = s.g.face[fi];
+    BcStageFace &c = set.fc[i];
+    c.tg = s.tab + (size_t)fi * 3 * s.ld * 2;
+    c.tk = s.tab + (size_t)(BcStage::kMaxFaces + fi) * 3 * s.ld * 2;
+    c.ld = s.ld;
+    c.kind = s.f.kind;
+    c.w = bc_sine_weights(s.f, F);
+    c.alpha = s.alpha;
+    c.c = s.f.prm[0];
+    set.offset[i] = F.offset;
+    set.Q0[i] = F.Q[0];
+    set.Q1[i] = F.Q[1];
+    q0 = std::max(q0, F.Q[0]);
+    q1 = std::max(q1, F.Q[1]);
+  }
+  if (q0 <= 0 || q1 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bc_stage_fill_kernel, dim3((unsigned)((q0 + 255) / 256), (unsigned)q1, (unsigned)n), dim3(256), 0,
+                     st, set, out);
   return hipGetLastError();
 }
 
