@@ -208,7 +208,7 @@ class GdmOperator:
 
     def apply_bc_fn(self, src_local, dst_owned, fn_kind, params, t_g, alpha=0.0, t_k=0.0):
         """apply() with the stage boundary values g(t_g) + alpha dg/dt(t_k) of a
-        built-in function evaluated inside the face kernels (gdm_apply_bc_fn):
+        built-in function computed by the engine right before the stencil (gdm_apply_bc_fn):
         the same bits as eval_boundary + rk_update + apply(bc_values)"""
         self._check_sizes(src_local, dst_owned)
         prm = (ctypes.c_double * max(len(params), 1))(*[float(v) for v in params])

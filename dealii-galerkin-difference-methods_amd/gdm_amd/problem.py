@@ -18,7 +18,7 @@ advection/stiffness.h:181-194) and dg/dt at the stage times
 (stiffness.h:286-289), both evaluated on the device for the built-in
 boundary functions.  By default block(0) is not stored at all: stage s reads
 y0 + h a_{s,s-1} k_{s-1} = g(t_n) + h a dg/dt(t_n + c_{s-1} h), which the
-face kernels evaluate where they read it (gdm_apply_bc_fn, the same bits as
+engine computes per stage itself (gdm_apply_bc_fn, the same bits as
 gdm_eval_boundary + gdm_vec_rk_update); block(0) after a step is never read
 by the reference (initialize_time_step overwrites it, problem.h:88-90).
 carry_bc=True keeps the explicit block(0) vectors (gdm_eval_boundary).
@@ -149,7 +149,7 @@ class AdvectionProblem:
     def step(self, t, h):
         op = self.op
         if not self.carry_bc:
-            # block(0) evaluated in the face kernels: stage s reads g(t) + alpha dg/dt(t_k)
+            # block(0) computed by the engine: stage s reads g(t) + alpha dg/dt(t_k)
             y, acc, Y, k = self.u, self._acc[1], self._Y[1], self._k[1]
             stage = y
             for s in range(4):

@@ -12,7 +12,7 @@
 // global order) and prints one line per step with |u|_2.  DEVBC = 1 evaluates
 // g and dg/dt on the device (GDM_FN_SINE_PRODUCT with the same parameters)
 // instead of the host callbacks, with the stage values of block(0) evaluated
-// inside the face kernels (Parameters::boundary_in_faces); DEVBC = 2 the same
+// by the engine per stage (Parameters::boundary_in_faces); DEVBC = 2 the same
 // function with block(0) stored and RK-updated.  NRANKS > 1 runs the multi-rank path: one
 // thread per rank (z-slabs of system.h:720-757, all on DEVICE), ghost planes
 // and dots through GDM::HIP::ThreadGroup (an MPI communicator's role), the

@@ -73,7 +73,7 @@ struct Parameters {
   int boundary_function = -1;
   std::vector<double> boundary_function_params;
   // with a built-in boundary function: evaluate the stage values of block(0)
-  // (g(t_n) + h a_{s,s-1} dg/dt) inside the face kernels (gdm_apply_bc_fn /
+  // (g(t_n) + h a_{s,s-1} dg/dt) in the engine, per stage (gdm_apply_bc_fn /
   // gdm_add_boundary_fn) instead of storing and RK-updating block(0); the
   // same bits for block(1); block(0) of the solution is then not maintained
   // (initialize_time_step overwrites it every step, problem.h:88-90)
@@ -321,10 +321,10 @@ class StiffnessMatrixOperator {
     }
   }
 
-  // block(0) from the built-in function inside the face kernels
+  // block(0) from the built-in function, computed by the engine per stage
   bool boundary_in_faces() const { return bc_fn >= 0 && layout.n_bc_points > 0; }
   // compute_rhs's block(1) with the stage boundary values g(t_g) + alpha
-  // dg/dt(t_k) evaluated where the face kernels read them (gdm_apply_bc_fn)
+  // dg/dt(t_k) computed by the engine per stage (gdm_apply_bc_fn)
   void compute_rhs_fn(DeviceVector &rhs_block1, const DeviceVector &u, double t_g, double alpha, double t_k) const {
     check(gdm_apply_bc_fn(op, u.get_values(), owned(rhs_block1), bc_fn, bc_fn_params.data(),
                           (int)bc_fn_params.size(), t_g, alpha, t_k),
@@ -561,7 +561,7 @@ class AdvectionProblem {
     if (params.n_ranks != 1) rhs_tmp.reinit(stiffness_matrix_operator.handle(), stiffness_matrix_operator.get_layout().n_owned);
     use_spike = params.n_ranks != 1 && mass_matrix_operator.spike_available();
     const bool in_faces = params.boundary_in_faces && stiffness_matrix_operator.boundary_in_faces();
-    // stage boundary values inside the face kernels: g(t0) + alpha dg/dt(t_k)
+    // stage boundary values computed by the engine: g(t0) + alpha dg/dt(t_k)
     double t0 = 0.0, bc_alpha = 0.0, bc_tk = 0.0;
     const auto fu_rhs = [&](double time, BlockVector &y, BlockVector &result) {
       if (in_faces) {

@@ -297,7 +297,8 @@ int gdm_vec_rk_update(gdm_op *op, int64_t n, double beta, const double *k, const
 int gdm_eval_boundary(gdm_op *op, int fn_kind, const double *params, int n_params, double t, int derivative,
                       double *bc_values);
 /* gdm_apply_bc_fn: gdm_apply (stencil + inflow boundary term) with the stage
- * boundary values evaluated inside the face kernels instead of read from a
+ * boundary values computed by the engine (into its own scratch, inflow faces
+ * only, one launch before the stencil) instead of read from a caller's
  * bc_values vector: BC = g(t_g) + alpha dg/dt(t_k) (alpha = 0: g(t_g)), the
  * same bits as gdm_eval_boundary(g, t_g) / (dg/dt, t_k) followed by
  * gdm_vec_rk_update's Y = y + alpha k.  This is block(0) of the reference's

@@ -1,5 +1,5 @@
 """gdm_apply_bc_fn (include/gdm_hip.h): the RK stage boundary values
-g(t_g) + alpha dg/dt(t_k) evaluated inside the face kernels give the same
+g(t_g) + alpha dg/dt(t_k) computed by the engine (gdm_apply_bc_fn) give the same
 bits as the explicit block(0) path of the reference's RK stages
 (advection/problem.h:62-94; gdm_eval_boundary + gdm_vec_rk_update +
 gdm_apply with the stage vector), and AdvectionProblem's default step (no

@@ -84,7 +84,7 @@ def test_driver_fails_loudly_without_gpu(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dim,p,n,steps,ranks", [(2, 5, 24, 3, 1), (3, 5, 12, 2, 1), (3, 5, 24, 2, 2)])
 def test_driver_boundary_in_faces_bitwise(tmp_path, dim, p, n, steps, ranks):
-    """devbc = 1 (block(0) stage values evaluated in the face kernels,
+    """devbc = 1 (block(0) stage values computed by the engine,
     gdm_apply_bc_fn / gdm_add_boundary_fn) and devbc = 2 (block(0) stored and
     RK-updated, gdm_eval_boundary + gdm_vec_rk_update) give the same bits"""
     u = []
