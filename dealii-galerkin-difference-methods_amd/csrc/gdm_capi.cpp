@@ -853,6 +853,36 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
   // order-dependent, which the bit-exact rank / communicator comparisons of
   // tests/test_host_mpi.py catch.
   const hipStream_t fst = (phase == 1 || phase == 3) && st ? st : op->stream;
+  if (phase == 4 && all_g && op->dim == 3) {
+    // all faces' adds in one launch, the same ordered sums per node
+    gdmk::FaceAddFace ff[kMax] = {};
+    int m = 0;
+    bool ok = true;
+    for (size_t fi = 0; fi < op->faces.size(); ++fi) {
+      const Face &F = op->faces[fi];
+      if (F.scale == 0.0) continue;
+      gdmk::FaceAddFace &a = ff[m++];
+      a.G = F.G;
+      a.base = F.base;
+      a.stride0 = F.t0.stride;
+      a.stride1 = F.t1.stride;
+      a.d = F.d;
+      a.plane = F.side ? (int)(op->N[F.d] - 1) : 0;
+      a.a0 = F.t0.dim_index;
+      a.b0 = F.t0.node_begin;
+      a.e0 = F.t0.node_end;
+      a.a1 = F.t1.dim_index;
+      a.b1 = F.t1.node_begin;
+      a.e1 = F.t1.node_end;
+      ok = ok && a.a0 >= 0 && a.a1 >= 0;
+    }
+    if (ok) {
+      const int64_t own_off = (int64_t)op->layout.owned_plane_begin * op->layout.plane_size;
+      const hipError_t e = gdmk_launch_face_adds(ff, m, op->N[0], op->N[1], own_off, dst_owned, op->stream);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotSupported) hip_check(e, "face adds");
+    }
+  }
   if (phase == 3 && all_g) {
     const hipError_t e = gdmk_launch_faces_g(fas, nf, fst);
     if (e == hipSuccess) return;

@@ -97,6 +97,15 @@ struct RkOut {
   double beta, alpha;
 };
 
+// phase-4 geometry of one inflow face (gdmk_launch_face_adds): normal axis d
+// at global node coordinate `plane`, tangential axes a0 / a1 (-1 = trivial)
+// with owned node ranges [b0, e0) / [b1, e1); G is [i1 - b1][i0 - b0]
+struct FaceAddFace {
+  const double *G;
+  int64_t base, stride0, stride1;  // owned index of node (b0, b1), index strides along a0 / a1
+  int d, plane, a0, b0, e0, a1, b1, e1;
+};
+
 constexpr int FACE_CHUNK = 256;  // t0 nodes per workgroup of the face row kernel
 
 // hipFuncAttributeMaxDynamicSharedMemorySize is a per-device property of a
@@ -149,6 +158,11 @@ hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st);
 // launches; hipErrorNotSupported unless every face uses the cell form of step 1
 // with its own T and G (the caller then launches face by face)
 hipError_t gdmk_launch_faces_g(const gdmk::FaceArgs *fa, int n, hipStream_t st);
+// phase 4 of n inflow faces in one launch: every face node gets dst += G of
+// each face containing it, in face order (the node's first face's thread does
+// all of its adds: the same sums as n ordered launches)
+hipError_t gdmk_launch_face_adds(const gdmk::FaceAddFace *f, int n, int64_t N0, int64_t N1, int64_t own_off,
+                                 double *dst, hipStream_t st);
 hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st);
 hipError_t gdmk_launch_dot(int64_t n, const double *x, const double *y, double *partial, int n_partial, double *out,
                            hipStream_t st);

@@ -1926,6 +1926,40 @@ __global__ void __launch_bounds__(256) face_step2_multi_kernel(const Step2Set se
   F.G[(int64_t)(i1 - F.i1_begin) * F.n0 + t] = face_step2_value(F.T, F.n0, t, i1, F.qs1, F.qc1, F.w1, F.wmax1, F.scale);
 }
 
+struct FaceAddSet {
+  FaceAddFace f[BcStage::kMaxFaces];
+  int n;
+  int64_t N0, N1, own_off;
+};
+__device__ __forceinline__ bool face_add_member(const FaceAddFace &g, const int c[3]) {
+  return c[g.d] == g.plane && (g.a0 < 0 || (c[g.a0] >= g.b0 && c[g.a0] < g.e0)) &&
+         (g.a1 < 0 || (c[g.a1] >= g.b1 && c[g.a1] < g.e1));
+}
+// one thread per node of face blockIdx.z; a node shared with an earlier face
+// is left to that face's thread, which adds every containing face's G in face
+// order: dst + G_f + G_g ..., the sums of the ordered per-face launches
+__global__ void __launch_bounds__(256) face_add_multi_kernel(const FaceAddSet set, double *__restrict__ dst) {
+  const int f = blockIdx.z;
+  const FaceAddFace &F = set.f[f];
+  const int n0 = F.e0 - F.b0;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x, i1 = blockIdx.y;
+  if (t >= n0 || i1 >= F.e1 - F.b1) return;
+  const int64_t o = F.base + (int64_t)t * F.stride0 + (int64_t)i1 * F.stride1;
+  const int64_t gi = o + set.own_off;
+  const int c[3] = {(int)(gi % set.N0), (int)((gi / set.N0) % set.N1), (int)(gi / (set.N0 * set.N1))};
+  for (int g = 0; g < f; ++g)
+    if (face_add_member(set.f[g], c)) return;
+  double v = dst[o];
+  v = v + F.G[(int64_t)i1 * n0 + t];
+  for (int g = f + 1; g < set.n; ++g) {
+    const FaceAddFace &H = set.f[g];
+    if (!face_add_member(H, c)) continue;
+    const int u0 = H.a0 < 0 ? 0 : c[H.a0] - H.b0, u1 = H.a1 < 0 ? 0 : c[H.a1] - H.b1;
+    v = v + H.G[(int64_t)u1 * (H.e0 - H.b0) + u0];
+  }
+  dst[o] = v;
+}
+
 // dst node (t, i1) += G[i1][t]: one launch per face, in face order
 __global__ void __launch_bounds__(256) face_add_kernel(const double *__restrict__ G, int n0, int n1,
                                                         double *__restrict__ dst, int64_t base, int64_t stride0,
@@ -2290,6 +2324,27 @@ static hipError_t faces_g_launch(const gdmk::FaceArgs *fa, int n, Get &&src, hip
     default: return hipErrorNotSupported;
   }
   hipLaunchKernelGGL(face_step2_multi_kernel, dim3(g2x, g2y, n), dim3(256), 0, st, s2);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t gdmk_launch_face_adds(const gdmk::FaceAddFace *f, int n, int64_t N0, int64_t N1,
+                                            int64_t own_off, double *dst, hipStream_t st) {
+  using namespace gdmk;
+  if (n <= 0) return hipSuccess;
+  if (n > BcStage::kMaxFaces || N0 <= 0 || N1 <= 0) return hipErrorNotSupported;
+  FaceAddSet set{};
+  set.n = n;
+  set.N0 = N0;
+  set.N1 = N1;
+  set.own_off = own_off;
+  int gx = 0, gy = 0;
+  for (int i = 0; i < n; ++i) {
+    set.f[i] = f[i];
+    gx = std::max(gx, (f[i].e0 - f[i].b0 + 255) / 256);
+    gy = std::max(gy, f[i].e1 - f[i].b1);
+  }
+  if (gx <= 0 || gy <= 0) return hipSuccess;
+  hipLaunchKernelGGL(face_add_multi_kernel, dim3(gx, gy, n), dim3(256), 0, st, set, dst);
   return hipGetLastError();
 }
 
