@@ -21,6 +21,12 @@ rk4_stage_ms).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment
+starts the N ranks itself (one child process per GPU with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set; the parent never touches
+the GPU) and exits with the first failing child's code.  Under torchrun the
+launcher's WORLD_SIZE must equal --gpus.
 """
 import argparse
 import json
@@ -304,6 +310,80 @@ def c4_rank_slab(steps=10, n_ranks=8, rank=3):
     return res
 
 
+def c3_rank_slab(steps=10, n_ranks=8, rank=3):
+    """C3 at its named 8-GPU split, one rank's share on this GPU: rank 3 of 8
+    of the 512^3 p = 5 advection grid (system.h:720-757: 64 owned + 2 x 5
+    ghost planes).  compute_rhs is timed as apply_overlapped runs it at N = 8
+    (advection/stiffness.h:343 update_ghost_values overlapped with the planes
+    that need no ghosts): the interior planes, the 2 x p edge planes, the
+    inflow data; the exchange itself needs a second GPU and is not part of
+    this figure.  The mass inverse is the distributed exact one of that rank
+    (truncated SPIKE: slab solve + interface correction, problem.h:236-267)."""
+    import torch
+    from gdm_amd import GdmOperator, _capi
+    from gdm_amd.distributed import apply_overlapped
+
+    op = GdmOperator(3, 5, 511, 0.0, 1.0, "advection", params=(1.0, 0.15, -0.05), n_ranks=n_ranks, rank=rank)
+    L = op.layout
+    gen = torch.Generator(device="cuda").manual_seed(20251013)
+    u = torch.rand(op.n_local, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+    v = op.new_vector(False)
+    bc = torch.rand(max(op.n_bc_points, 1), dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+    p = L["halo_depth"]
+    pb, pe = L["owned_plane_begin"], L["owned_plane_end"]
+    lo = pb + (p if L["ghost_planes_below"] else 0)
+    hi = pe - (p if L["ghost_planes_above"] else 0)
+
+    def timed(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / steps
+
+    whole = timed(lambda: apply_overlapped(op, None, u, v, bc if op.n_bc_points else None))
+    interior = timed(lambda: op.apply_planes(u, v, lo, hi))
+
+    def edges():
+        op.apply_planes(u, v, pb, lo)
+        op.apply_planes(u, v, hi, pe)
+
+    edge = timed(edges)
+    rounds = _capi.mesh_spike_rounds(op.mesh)
+    x = op.new_vector(True)
+    r = v.clone()
+
+    def solve():
+        op.mass_solve_slab(r, op.owned_view(x))
+        for k in range(rounds):
+            op.mass_solve_interface_round(x, k)
+        op.mass_solve_interface(x)
+
+    spike = timed(solve)
+    N = op.n_owned
+    n_int = (hi - lo) * L["plane_size"]
+    res = {
+        "workload": "C3 rank %d of %d: 512^2 x %d owned planes + %d + %d ghost planes, p=5 advection"
+                    % (rank, n_ranks, pe - pb, L["ghost_planes_below"], L["ghost_planes_above"]),
+        "n_dofs_rank": N,
+        "compute_rhs_ms": whole,
+        "interior_planes_ms": interior,
+        "edge_planes_ms": edge,
+        "stencil_frac": BYTES_PER_DOF * N / (whole * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "interior_frac": BYTES_PER_DOF * n_int / (interior * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "spike_solve_ms": spike,
+        "spike_rounds": rounds,
+        "mass_solve_frac": BYTES_PER_DOF * N / (spike * 1e-3) / 1e9 / HBM_PEAK_GBS,
+    }
+    del op, u, v, x, r, bc
+    torch.cuda.empty_cache()
+    return res
+
+
 def _nproc():
     try:
         return len(os.sched_getaffinity(0))
@@ -389,8 +469,60 @@ def pmc_traffic(args):
     return (2.0 * res["FETCH_SIZE"] + res["WRITE_SIZE"]) * 1024.0
 
 
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n, cmd, env=None, poll_s=0.2):
+    """Run `cmd` as n rank processes of one job on this node (one per GPU):
+    each child gets RANK = LOCAL_RANK = r, WORLD_SIZE = n, MASTER_ADDR =
+    127.0.0.1 and a free MASTER_PORT, and inherits stdout / stderr (rank 0
+    prints the JSON line).  Returns 0 when every child exits 0, else the first
+    non-zero exit code seen (a child killed by signal s gives 128 + s); the
+    other children are then terminated by PID, so that none is left waiting in
+    a collective.  The caller must not have touched the GPU."""
+    base = dict(os.environ if env is None else env)
+    base.update({"WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port())})
+    procs = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(n)})
+        procs.append(subprocess.Popen(cmd, env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        for pr in list(live):
+            c = pr.poll()
+            if c is None:
+                continue
+            live.remove(pr)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for other in live:
+                    other.terminate()
+        time.sleep(poll_s)
+    return rc
+
+
+def rank_command(argv):
+    """the command of one rank started by `bench.py --gpus N`: this script
+    with the parent's arguments (the child sees WORLD_SIZE and runs its rank)"""
+    return [sys.executable, os.path.abspath(__file__)] + list(argv)
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # no launcher: start the ranks here (before anything initialises the GPU)
+        sys.exit(spawn_ranks(args.gpus, rank_command(sys.argv[1:])))
+    if world_env is not None and int(world_env) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d" % (world_env, args.gpus), file=sys.stderr)
+        sys.exit(2)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -501,8 +633,9 @@ def main():
             torch.cuda.synchronize()
             stage_ms = e0.elapsed_time(e1) / 12.0
             del prob
-    c4 = None
+    c4 = c3r = None
     if world == 1 and not args.metric_only:
+        c3r = c3_rank_slab()
         c4 = c4_wave_stage()
     traffic = None
     if world == 1 and str(args.pmc) == "1" and not args.metric_only:
@@ -552,6 +685,7 @@ def main():
             "mass_solve": mass,
         },
         "rk4_stage_ms": stage_ms,
+        "c3_per_rank_8": c3r,
         "c4_wave": c4,
         "cpu_baseline": cpu,
     }

@@ -739,13 +739,6 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
     a.corrX = op->corrX;
     a.zt = op->zt;
   }
-#ifdef GDM_DIAG
-  if (const char *env = std::getenv("GDM_DBG")) a.dbg = std::atoi(env);
-#endif
-#ifdef GDM_STAMP
-  a.stamps = nullptr;
-  if (const char *env = std::getenv("GDM_STAMP_PTR")) a.stamps = (unsigned long long *)std::strtoull(env, nullptr, 0);
-#endif
   if (L.n_owned == 0) return hipSuccess;
   const int bk = as_mass ? 0 : (op->kind == GDM_OP_WAVE ? 2 : 1);
   if (!v8) {

@@ -52,11 +52,6 @@ struct StencilArgs {
   // v8 only: output plane ranges computed by this launch (chunks of zchunk
   // planes; blockIdx.z < nchunk0 -> range 0, else range 1)
   int cz0[2], cz1[2], nchunk0;
-  int dbg;  // diagnostic builds only (-DGDM_DIAG): bits disable kernel phases
-#ifdef GDM_STAMP
-  // stamp builds only: s_memtime per wave and phase, planes [STAMP_I0, +STAMP_NI)
-  unsigned long long *stamps;
-#endif
 };
 
 // Inflow boundary-data projection of one box face (two tangential directions

@@ -45,11 +45,6 @@
 // nt) and its output stores (1 = non-temporal).  A/B at C3 on the MI355X
 // (profiles/r3x, 3 repetitions each): cached 0.840-0.849 ms, non-temporal
 // stores 0.822-0.837 ms (the default), non-temporal stores and DMA 0.835-0.845
-// producers issue the next plane's DMA per row group right after reading the
-// group's window (before its FMAs) instead of after the whole x-sweep
-#ifndef GDM_EARLY_DMA
-#define GDM_EARLY_DMA 0
-#endif
 #ifndef GDM_STENCIL_LD_CPOL
 #define GDM_STENCIL_LD_CPOL 0
 #endif
@@ -67,36 +62,7 @@ namespace gdmk {
 
 
 #define GDM_WAIT_VMCNT(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
-#ifdef GDM_DIAG
-#define GDM_DBG(a, bit) (((a).dbg & (bit)) != 0)
-#else
-#define GDM_DBG(a, bit) false
-#endif
 #define GDM_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
-// stamp builds (-DGDM_STAMP, tools/stamp_stencil.py): s_memtime of every wave
-// at the phase boundaries of planes [STAMP_I0, STAMP_I0 + STAMP_NI) of every
-// workgroup, stored by lane 0 (vector store) to a.stamps[((sid * NI + i) *
-// 16 + wave) * 8 + slot].  Timing shares only: the stamps' waits change the
-// kernel.
-#ifdef GDM_STAMP
-#define STAMP_I0 40
-#define STAMP_NI 24
-#define GDM_STAMPT(t_, i_, slot_)                                                                    \
-  do {                                                                                               \
-    if (a.stamps && (i_) >= STAMP_I0 && (i_) < STAMP_I0 + STAMP_NI) {                                \
-      unsigned long long ts_;                                                                        \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");                      \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-      if ((t_).lane == 0)                                                                            \
-        a.stamps[(((int64_t)(t_).sid * STAMP_NI + ((i_)-STAMP_I0)) * 16 + (t_).wv) * 8 + (slot_)] = ts_; \
-    }                                                                                                \
-  } while (0)
-#else
-#define GDM_STAMPT(t_, i_, slot_) \
-  do {                            \
-  } while (0)
-#endif
 
 // Coefficient tables are read-only for the whole launch and indexed by
 // wave-uniform positions: read them through the constant address space so
@@ -170,6 +136,7 @@ struct Dma7 {
 };
 
 typedef __attribute__((address_space(3))) double ldouble;
+typedef __attribute__((address_space(3))) unsigned int lu32;
 typedef double dpair __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) dpair ldouble2;
 typedef __attribute__((address_space(3))) const double lcdouble;
@@ -185,9 +152,10 @@ typedef __attribute__((address_space(3))) const dpair lcdouble2;
 
 struct Tile7 {
   ldouble *u0, *ab0, *zt, *yc, *corr, *yw;
-  int sid;  // stamp builds: logical workgroup id
-  int cw;   // v8 / v9: this wave's output row block (rows cw R .. cw R + R - 1 of the tile)
+  lu32 *sync;  // v8: hand-off counters
+  int cw;      // v8: this wave's output row block (rows cw R .. cw R + R - 1 of the tile)
   bool yedge;  // v8: the tile has rows next to a y wall
+  int ry0;     // v8 y-wall tiles: first tile row of the column table (yb - y0)
   int lane, wv, x0, y0, zc0, zc1, zs, ze, zend;
   // x wall columns inside this tile: nl from the left wall, nr from column rs on
   int nl, rs, ncw;
@@ -295,33 +263,6 @@ __device__ __forceinline__ void stage_plane_pre7(const StencilArgs &a, const Til
           else
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, d.vo[ps][i], 0, 0, GDM_STENCIL_LD_CPOL);
         }
-      }
-    }
-  }
-}
-
-// the DMA of one pass (row group t.wv + ps NP) of plane zz
-template <int P, int R, int NC, int NP, int BK, int CH>
-__device__ __forceinline__ void stage_pass_pre7(const StencilArgs &a, const Tile7 &t, int zz, ldouble *ubuf,
-                                                const DmaPre7<P, R, NC, NP, BK, CH> &d, int ps) {
-  using G = Geom7<P, R, NC, NP, BK>;
-  using S = Dma7<P, R, NC, NP, BK, CH>;
-  const int ny_in = a.in_y1 - a.in_y0;
-  const double *plane = a.src + (int64_t)(zz - a.in_z0) * ny_in * a.Nx;
-  const int nbytes = (int)((int64_t)ny_in * a.Nx * 8);
-  __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)plane, 0, nbytes, 0x00020000);
-  const int g = t.wv + ps * NP;
-  if (g < G::NG) {
-    const int ni = g == G::NG - 1 ? S::NI_LAST : S::NI_FULL;
-    auto *gbase = (__attribute__((address_space(3))) char *)(ubuf + g * 4 * G::RL);
-#pragma unroll
-    for (int i = 0; i < S::NI_FULL; ++i) {
-      if (i < ni && d.vo[ps][i] != 0xffffffffu) {
-        auto *dst = (__attribute__((address_space(3))) void *)(gbase + i * 64 * CH);
-        if constexpr (CH == 16)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, d.vo[ps][i], 0, 0, GDM_STENCIL_LD_CPOL);
-        else
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 4, d.vo[ps][i], 0, 0, GDM_STENCIL_LD_CPOL);
       }
     }
   }
@@ -481,13 +422,8 @@ __device__ __forceinline__ void cplane7(const StencilArgs &a, const Tile7 &t, bo
   constexpr int W = G::W;
   double D[R], E[R];
   if (zz < t.ze) {
-    if (GDM_DBG(a, 1)) {
-#pragma unroll
-      for (int j = 0; j < R; ++j) D[j] = E[j] = (double)zz;
-    } else {
-      ysweep7<P, R, NC, NP, BK>(a, t, ytoep, ybase, t.ab0 + ((zz - t.zs) & 1) * G::ABSZ, D, E);
-    }
-    if (!GDM_DBG(a, 16)) GDM_LDS_BARRIER();
+    ysweep7<P, R, NC, NP, BK>(a, t, ytoep, ybase, t.ab0 + ((zz - t.zs) & 1) * G::ABSZ, D, E);
+    GDM_LDS_BARRIER();
   } else {
 #pragma unroll
     for (int j = 0; j < R; ++j) D[j] = E[j] = 0.0;
@@ -495,7 +431,6 @@ __device__ __forceinline__ void cplane7(const StencilArgs &a, const Tile7 &t, bo
   const int row = zz < W ? zz : (zz >= a.Nz - W && zz < a.Nz ? W + zz - (a.Nz - W) : 2 * W);
   lcdouble2 *zc = (lcdouble2 *)t.zt + row * W;
   dpair cur = zc[0];
-  if (!GDM_DBG(a, 2)) {
 #pragma unroll
   for (int k = 0; k < W; ++k) {
     GDM_FENCE();
@@ -510,11 +445,9 @@ __device__ __forceinline__ void cplane7(const StencilArgs &a, const Tile7 &t, bo
     }
     cur = nxt;
   }
-  }
   // The ring values only feed the conditional retire stores; without this
   // opaque use LLVM sinks each slot's whole FMA chain into its store branch
   // and keeps every plane's D/E and coefficients alive until then.
-  GDM_STAMPT(t, zz - t.zs, 3);
 #pragma unroll
   for (int s = 0; s < W; ++s)
 #pragma unroll
@@ -536,7 +469,6 @@ __device__ __forceinline__ void cplane7(const StencilArgs &a, const Tile7 &t, bo
   }
 #pragma unroll
   for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
-  GDM_STAMPT(t, zz - t.zs, 4);
 }
 
 template <int JP, int P, int R, int NC, int NP, int BK>
@@ -571,20 +503,18 @@ __device__ __forceinline__ void producer7(const StencilArgs &a, const Tile7 &t) 
   for (int zz = t.zs; zz < t.ze; ++zz) {
     const int q = zz + 1;  // plane swept in this iteration
     if (q < t.ze) {
-      if (GDM_DBG(a, 8))
-        ;
-      else if (q + 1 < t.ze)
+      if (q + 1 < t.ze)
         wait_dma_plane<0, P, R, NC, NP, BK, CH>(t.wv);
       else
         GDM_WAIT_VMCNT(0);
       const int s = (q - t.zs) & 1;
-      if (!GDM_DBG(a, 4)) xsweep7<P, R, NC, NP, BK>(a, t, u[s], t.ab0 + s * G::ABSZ);
-      if (q + 2 < t.ze && !GDM_DBG(a, 8)) {
+      xsweep7<P, R, NC, NP, BK>(a, t, u[s], t.ab0 + s * G::ABSZ);
+      if (q + 2 < t.ze) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         stage_plane7<P, R, NC, NP, BK, CH>(a, t, q + 2, u[s]);
       }
     }
-    if (!GDM_DBG(a, 16)) GDM_LDS_BARRIER();
+    GDM_LDS_BARRIER();
   }
 }
 
@@ -650,19 +580,23 @@ __global__ void __launch_bounds__(64 * (NP + NC), (64 * (NP + NC)) / 256) stenci
 }
 
 // ===========================================================================
-// Fused Kronecker stencil, v8.  Same roles and tiles as v7, re-balanced for
-// latency:
-//   * each producer wave keeps a 3-slot LDS-DMA ring of its own row groups,
-//     so two planes are in flight at every wait (v7: one),
-//   * the x-sweep results stay in registers until the single interleaved
-//     (A, B) plane buffer is free; two barriers per plane:
-//       producer  X(i) | F_i | write AB(i) | L_i | DMA(i + 3)
-//       consumer  L_i | Y(i) | F_i+1 | Z(i)
-//     (X(i+1) overlaps Y(i), the AB write overlaps Z(i)),
-//   * consumers read (A, B) pairs with one ds_read_b128, PF rows ahead,
+// Fused Kronecker stencil, v8.  Same roles and tiles as v7:
+//   * each producer wave DMAs its own row groups of the (TY + 2p) x (64 + 2p)
+//     plane into a 2-slot LDS ring (a counted vmcnt keeps the next plane in
+//     flight) and x-sweeps them straight into the (A, B) plane buffer i & 1,
+//   * consumers read (A, B) pairs with one ds_read_b128, PF rows ahead, and
+//     scatter into a register ring of 2p + 1 output planes,
 //   * interior z planes use the compile-time bands (E arrives pre-scaled by
 //     the z mass scale, D is scaled by dint): no LDS reads in the z phase;
 //     only the 2(2p+1) wall planes read the LDS column table.
+// The roles hand over the (A, B) planes through counters in LDS instead of a
+// workgroup barrier per plane (the barrier serialised them):
+//   FULL[s]  producers, after their rows of the plane in slot s are stored,
+//   FREE[s]  consumers, once their reads of slot s have returned,
+//   YWF      producers of a y-wall tile, after their y-wall corrections,
+//   YWR      consumers, after reading the corrections (single-buffered only).
+// Counters only grow; a wave waits for the count the plane needs, so waves
+// of one role drift against each other and every SIMD keeps issuing.
 // ===========================================================================
 template <int P, int R, int NC, int NP, int BK>
 struct Geom8 {
@@ -691,26 +625,72 @@ struct Geom8 {
   static __device__ __forceinline__ int sw(int x) { return x ^ ((x >> 3) & 3); }
   static __device__ __forceinline__ int ab(int r, int x) { return NAB == 2 ? r * ABRS + 2 * sw(x) : r * TX + x; }
   static constexpr int ZTSZ = (2 * W + 1) * W * 2;  // wall planes + interior row
-  static constexpr int YCSZ = UR * W * 2;
+  // y-wall column tables: the tile rows [yb - y0, yb - y0 + YCR) that feed the
+  // (at most p + 1) wall rows of the tile's one y wall
+  static constexpr int YCR = 3 * P + 1;
+  static constexpr int YCSZ = YCR * W * 2;
   static constexpr int CORRSZ = 2 * (P + 1) * 2 * W;
   static constexpr int NWIN = 2 * P + 6;
-  // workgroups per CU the tile is sized for (<= 12 waves: two) and the DMA
-  // ring depth that fits that LDS share (3 slots if possible, else 2)
+  // workgroups per CU the tile is sized for (<= 12 waves: two)
   static constexpr int WGS = NW <= 12 ? 2 : 1;
   static constexpr size_t LDS_CAP = (160 * 1024) / WGS;
   // double-buffered (A, B) planes, 2-slot DMA ring (the single-buffered
-  // handoff with two barriers per plane and a 3-slot ring measured slower,
-  // also at two 8-wave workgroups per CU: profiles/r2_early, r3g)
+  // handoff and a 3-slot ring measured slower: profiles/r2_early, r3g)
   static constexpr int NSLOT = 2;
   static constexpr int NABUF = 2;
   static constexpr int YWSZ = (P + 1) * TX * NAB;  // y-wall corrections of one plane
+  static constexpr int NSYNC = 8;                  // 32-bit hand-off counters (SY_*)
   static constexpr int OFF_AB = NSLOT * USZ;
   static constexpr int OFF_ZT = OFF_AB + NABUF * ABSZ;
   static constexpr int OFF_YC = OFF_ZT + ZTSZ;
   static constexpr int OFF_CORR = OFF_YC + YCSZ;
-  static constexpr int OFF_YW = OFF_CORR + CORRSZ;
-  static constexpr size_t lds_bytes() { return sizeof(double) * (size_t)(OFF_YW + YWSZ); }
+  static constexpr int OFF_SYNC = OFF_CORR + CORRSZ;
+  static constexpr int OFF_YW = OFF_SYNC + NSYNC / 2;
+  // y-wall corrections double-buffered where the LDS has room (p <= 7), else
+  // one buffer and the producers wait for the consumers' reads (YWR)
+  static constexpr int NYW = sizeof(double) * (size_t)(OFF_YW + 2 * YWSZ) <= LDS_CAP ? 2 : 1;
+  static constexpr size_t lds_bytes() { return sizeof(double) * (size_t)(OFF_YW + NYW * YWSZ); }
 };
+
+// LDS hand-off counters of the v8 stencil (indices into Tile7::sync)
+enum { SY_FULL = 0, SY_FREE = 2, SY_YWF = 4, SY_YWR = 5 };
+
+// wait until counter c has reached target (wave-uniform).  One asm block,
+// spin included: a loop the compiler can see splits the live ranges of the
+// consumers' register ring around it (158 VGPRs spilled to scratch); the
+// spin sleeps between polls so that it takes few issue slots from the
+// working waves
+__device__ __forceinline__ void sync_wait(lu32 *c, unsigned target) {
+  unsigned v, sv;
+  asm volatile(
+      "1:\n\t"
+      "ds_read_b32 %0, %2\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_readfirstlane_b32 %1, %0\n\t"
+      "s_cmp_ge_u32 %1, %3\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_sleep 1\n\t"
+      "s_branch 1b\n"
+      "2:"
+      : "=&v"(v), "=&s"(sv)
+      : "v"((unsigned)(uintptr_t)c), "s"(target)
+      : "memory", "scc");
+}
+
+// count this wave (one lane) in counter c once its LDS accesses so far have
+// completed (stores landed, reads returned)
+__device__ __forceinline__ void sync_signal(lu32 *c) {
+  unsigned long long ex;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "ds_add_u32 %1, %2\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(ex)
+      : "v"((unsigned)(uintptr_t)c), "v"(1u)
+      : "memory");
+}
 
 // the z-direction interior band of operator kind BK (column form index 2p - k)
 template <int P, int BK>
@@ -913,10 +893,10 @@ __device__ __forceinline__ int ywall_end(const StencilArgs &a, int y0) {
   return min(y0 + TY, a.Ny);
 }
 
-// y-wall corrections of plane AB (edge tiles only, between L_i and M_i): for
-// the wall rows y of this tile dD(y) = sum_s c1(y, s) A(s) and
-// dE(y) = sum_s c1 B(s) + c3 A(s) with the (wall - Toeplitz) column tables;
-// one row per producer wave, lane = x
+// y-wall corrections of the (A, B) plane in t.ab0 (y-wall tiles only, once
+// every producer's rows of the plane are stored): for the wall rows y of this
+// tile dD(y) = sum_s c1(y, s) A(s) and dE(y) = sum_s c1 B(s) + c3 A(s) with the
+// (wall - Toeplitz) column tables, into t.yw; one row per producer wave, lane = x
 template <int P, int R, int NC, int NP, int BK>
 __device__ __forceinline__ void ywall8(const StencilArgs &a, const Tile7 &t) {
   using G = Geom8<P, R, NC, NP, BK>;
@@ -930,7 +910,7 @@ __device__ __forceinline__ void ywall8(const StencilArgs &a, const Tile7 &t) {
 #pragma unroll
     for (int k = 0; k < W; ++k) {
       const int rs = y + 2 * P - k - t.y0;  // tile row of input s = y + p - k
-      const dpair c = ((lcdouble2 *)t.yc)[rs * W + k];
+      const dpair c = ((lcdouble2 *)t.yc)[(rs - t.ry0) * W + k];
       if constexpr (BK != 0) {
         const dpair v = *(lcdouble2 *)(t.ab0 + G::ab(rs, t.lane));
         dD = fma(c.x, v.x, dD);
@@ -946,87 +926,57 @@ __device__ __forceinline__ void ywall8(const StencilArgs &a, const Tile7 &t) {
   }
 }
 
+// producer wave, plane i:
+//   wait DMA(i) | wait FREE[i & 1] (consumers done with plane i - 2) |
+//   X(i) -> (A, B) buffer i & 1 | FULL[i & 1] | DMA(i + 2) into the u slot just read |
+//   [y-wall tile: wait FULL (all producers) | ywall(i) | YWF]
 template <int P, int R, int NC, int NP, int BK, int CH>
 __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) {
   using G = Geom8<P, R, NC, NP, BK>;
-  // plane i: X(i) straight into (A, B) buffer i & 1 | B_i | [y walls: ywall(i) | M_i] | DMA(i + 2)
-  // (the buffer was last read by the consumers' Y(i - 2), before they reached B_(i-1))
-  {
-    ldouble *u[2] = {t.u0, t.u0 + G::USZ};
-    const int n = t.ze - t.zs;
-    DmaPre7<P, R, NC, NP, BK, CH> dpre;
-    stage_pre7<P, R, NC, NP, BK, CH>(a, t, dpre);
+  ldouble *u[2] = {t.u0, t.u0 + G::USZ};
+  const int n = t.ze - t.zs;
+  DmaPre7<P, R, NC, NP, BK, CH> dpre;
+  stage_pre7<P, R, NC, NP, BK, CH>(a, t, dpre);
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (k < n) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + k, u[k], dpre);
-    GDM_LDS_BARRIER();  // tables in LDS
-    dpair V1[4];
-    XWallPre<P, BK> xpre;
-    if (t.ncw > 0) xwall8_pre<P, R, NC, NP, BK>(a, t, xpre);
-    for (int i = 0; i < n; ++i) {
-      const int slot = i & 1;
-      GDM_STAMPT(t, i, 0);
-      if (GDM_DBG(a, 8))
-        ;
-      else if (i + 1 < n)
-        wait_dma_planes<0, 1, P, R, NC, NP, BK, CH>(t.wv);
-      else
-        GDM_WAIT_VMCNT(0);
-      Tile7 tt = t;
-      tt.ab0 = t.ab0 + slot * G::ABSZ;
-      GDM_STAMPT(t, i, 1);
-#if GDM_EARLY_DMA
-      // per row group: read the group's window (and x-wall taps) from the u
-      // slot, then issue DMA(i + 2) of the group into the rows just read,
-      // then the FMAs -- the next plane's fetch starts one x-sweep earlier
+  for (int k = 0; k < 2; ++k)
+    if (k < n) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + k, u[k], dpre);
+  GDM_LDS_BARRIER();  // tables in LDS, counters zeroed
+  dpair V1[4];
+  XWallPre<P, BK> xpre;
+  if (t.ncw > 0) xwall8_pre<P, R, NC, NP, BK>(a, t, xpre);
+  for (int i = 0; i < n; ++i) {
+    const int slot = i & 1;
+    if (i + 1 < n)
+      wait_dma_planes<0, 1, P, R, NC, NP, BK, CH>(t.wv);
+    else
+      GDM_WAIT_VMCNT(0);
+    Tile7 tt = t;
+    tt.ab0 = t.ab0 + slot * G::ABSZ;
+    tt.yw = t.yw + (G::NYW == 2 ? slot : 0) * G::YWSZ;
+    sync_wait(t.sync + SY_FREE + slot, NC * (i >> 1));
 #pragma unroll
-      for (int ps = 0; ps < G::NPASS; ++ps) {
-        const int g = t.wv + ps * NP;
-        if (g < G::NG) {
-          double w[G::NWIN];
-          xload8<P, R, NC, NP, BK>(tt, u[slot], g, w);
+    for (int ps = 0; ps < G::NPASS; ++ps) {
+      const int g = t.wv + ps * NP;
+      if (g < G::NG) {
+        xsweep8<P, R, NC, NP, BK>(a, tt, u[slot], g, V1);
+        write_ab8<P, R, NC, NP, BK>(tt, g, V1);
+        if (t.ncw > 0) {
           XWall<P, BK> xw0;
-          if (t.ncw > 0) xwall8_calc<P, R, NC, NP, BK>(tt, u[slot], g, xpre, xw0);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (i + 2 < n && !GDM_DBG(a, 8)) stage_pass_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre, ps);
-          xcalc8<P, R, NC, NP, BK>(a, w, V1);
-          if (!GDM_DBG(a, 64)) write_ab8<P, R, NC, NP, BK>(tt, g, V1);
-          if (t.ncw > 0) xwall8_add<P, BK>(tt, xw0);
+          xwall8_calc<P, R, NC, NP, BK>(tt, u[slot], g, xpre, xw0);
+          xwall8_add<P, BK>(tt, xw0);
         }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      GDM_STAMPT(t, i, 2);
-      GDM_STAMPT(t, i, 3);
-#else
-#pragma unroll
-      for (int ps = 0; ps < G::NPASS; ++ps) {
-        const int g = t.wv + ps * NP;
-        if (g < G::NG) {
-          if (!GDM_DBG(a, 4)) xsweep8<P, R, NC, NP, BK>(a, tt, u[slot], g, V1);
-          if (!GDM_DBG(a, 64)) write_ab8<P, R, NC, NP, BK>(tt, g, V1);
-          if (t.ncw > 0) {
-            XWall<P, BK> xw0;
-            xwall8_calc<P, R, NC, NP, BK>(tt, u[slot], g, xpre, xw0);
-            xwall8_add<P, BK>(tt, xw0);
-          }
-        }
-      }
-      // DMA(i + 2) into this wave's own rows of slot i & 1 as soon as its own
-      // reads of them have returned (before B_i: the barrier wait then
-      // overlaps the fetch)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      GDM_STAMPT(t, i, 2);
-      if (i + 2 < n && !GDM_DBG(a, 8)) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre);
-      GDM_STAMPT(t, i, 3);
-#endif
-      if (!GDM_DBG(a, 16)) GDM_LDS_BARRIER();  // B_i: AB(i) complete
-      GDM_STAMPT(t, i, 4);
-      if (t.yedge) {
-        ywall8<P, R, NC, NP, BK>(a, tt);
-        GDM_LDS_BARRIER();  // M_i
       }
     }
-    return;
+    // (the wait in sync_signal also orders this wave's reads of the u slot
+    // before the DMA that overwrites it)
+    sync_signal(t.sync + SY_FULL + slot);
+    if (i + 2 < n) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre);
+    if (t.yedge) {
+      sync_wait(t.sync + SY_FULL + slot, NP * ((i >> 1) + 1));
+      if constexpr (G::NYW == 1) sync_wait(t.sync + SY_YWR, NC * i);
+      ywall8<P, R, NC, NP, BK>(a, tt);
+      sync_signal(t.sync + SY_YWF);
+    }
   }
 }
 
@@ -1080,418 +1030,47 @@ __device__ __forceinline__ void ysweep8(const StencilArgs &a, const Tile7 &t, do
   }
 }
 
+// consumer wave, input plane zz (index i = zz - zs):
+//   wait FULL[i & 1] | Y(i) [+ y-wall corrections after YWF] | FREE[i & 1] |
+//   Z(i) | retire output plane zz - p
 template <int JP, int P, int R, int NC, int NP, int BK, int PF, bool WALL, bool YW>
-__device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, int ybase, bool full,
+__device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, int ybase, bool full, bool ywave,
                                         double (&acc)[2 * P + 1][R], int zz) {
   using G = Geom8<P, R, NC, NP, BK>;
   using IR = InteriorRows<P>;
   constexpr int W = G::W;
   if (zz < t.ze) {
+    const int i = zz - t.zs, bs = i & 1;  // (A, B) buffer of the plane
     double D[R], E[R];
-    GDM_STAMPT(t, zz - t.zs, 0);
-    GDM_LDS_BARRIER();  // L_i (DB: B_i)
-    GDM_STAMPT(t, zz - t.zs, 1);
+    sync_wait(t.sync + SY_FULL + bs, NP * ((i >> 1) + 1));
     Tile7 tt = t;
-    tt.ab0 = t.ab0 + ((zz - t.zs) & 1) * G::ABSZ;
-    if (GDM_DBG(a, 1)) {
-#pragma unroll
-      for (int j = 0; j < R; ++j) D[j] = E[j] = (double)zz;
-    } else {
-      ysweep8<P, R, NC, NP, BK, PF>(a, tt, D, E);
-    }
-    GDM_STAMPT(t, zz - t.zs, 2);
+    tt.ab0 = t.ab0 + bs * G::ABSZ;
+    ysweep8<P, R, NC, NP, BK, PF>(a, tt, D, E);
     if constexpr (YW) {
-      GDM_LDS_BARRIER();  // M_i
-      const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
+      if (ywave) {
+        sync_wait(t.sync + SY_YWF, NP * (i + 1));
+        const ldouble *yw = t.yw + (G::NYW == 2 ? bs : 0) * G::YWSZ;
+        const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
 #pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const int y = ybase + j;
-        if (y >= yb && y < ye) {
-          if constexpr (BK != 0) {
-            const dpair c = ((lcdouble2 *)t.yw)[(y - yb) * G::TX + t.lane];
-            D[j] += c.x;
-            E[j] += c.y;
-          } else {
-            D[j] += t.yw[(y - yb) * G::TX + t.lane];
+        for (int j = 0; j < R; ++j) {
+          const int y = ybase + j;
+          if (y >= yb && y < ye) {
+            if constexpr (BK != 0) {
+              const dpair c = ((lcdouble2 *)yw)[(y - yb) * G::TX + t.lane];
+              D[j] += c.x;
+              E[j] += c.y;
+            } else {
+              D[j] += yw[(y - yb) * G::TX + t.lane];
+            }
           }
         }
       }
+      if constexpr (G::NYW == 1) sync_signal(t.sync + SY_YWR);
     }
-    if (!GDM_DBG(a, 2)) {
-      if constexpr (!WALL) {
-        // interior z column: out += mhat[k] E + zd[k] D with zd = dint dhat[2p - k]
-        // (the scale folded into the coefficients; zd[p] = 0 for advection)
-#pragma unroll
-        for (int k = 0; k < W; ++k) {
-          GDM_FENCE();
-          const int slot = (JP - P + k + 2 * W) % W;
-#pragma unroll
-          for (int j = 0; j < R; ++j) {
-            if constexpr (BK == 0)
-              acc[slot][j] = fma(hcoef<P, BK>(a.zd, k), D[j], acc[slot][j]);
-            else if (zband<P, BK>(k) == 0.0)
-              acc[slot][j] = fma(IR::m[k], E[j], acc[slot][j]);
-            else
-              acc[slot][j] = fma(IR::m[k], E[j], fma(hcoef<P, BK>(a.zd, k), D[j], acc[slot][j]));
-          }
-        }
-      } else {
-        // wall blocks: every plane from the column table (row 2W = interior)
-        const int row = zz < W ? zz : (zz >= a.Nz - W ? W + zz - (a.Nz - W) : 2 * W);
-#ifdef GDM_EXP_SZT
-        cdouble *zg = cptr(a.zt) + row * W * 2;
-#pragma unroll
-        for (int k = 0; k < W; ++k) {
-          const double ce = zg[2 * k], cd = zg[2 * k + 1];
-          const int slot = (JP - P + k + 2 * W) % W;
-#pragma unroll
-          for (int j = 0; j < R; ++j) {
-            if constexpr (BK == 0)
-              acc[slot][j] = fma(cd, D[j], acc[slot][j]);
-            else
-              acc[slot][j] = fma(ce, E[j], fma(cd, D[j], acc[slot][j]));
-          }
-        }
-        if (false) {
-#else
-        {
-#endif
-        lcdouble2 *zc = (lcdouble2 *)t.zt + row * W;
-        dpair cur = zc[0];
-#pragma unroll
-        for (int k = 0; k < W; ++k) {
-          GDM_FENCE();
-          const dpair nxt = zc[k + 1 < W ? k + 1 : k];
-          const int slot = (JP - P + k + 2 * W) % W;
-#pragma unroll
-          for (int j = 0; j < R; ++j) {
-            if constexpr (BK == 0)
-              acc[slot][j] = fma(cur.y, D[j], acc[slot][j]);
-            else
-              acc[slot][j] = fma(cur.x, E[j], fma(cur.y, D[j], acc[slot][j]));
-          }
-          cur = nxt;
-        }
-        }
-      }
-    }
-  }
-  GDM_STAMPT(t, zz - t.zs, 3);
-#pragma unroll
-  for (int s = 0; s < W; ++s)
-#pragma unroll
-    for (int j = 0; j < R; ++j) asm volatile("" : "+v"(acc[s][j]));
-  // retire output plane zz - p
-  constexpr int rslot = (JP - P + 2 * W) % W;
-  const int zo = zz - P;
-  if (zo >= t.zc0 && zo < t.zc1 && !GDM_DBG(a, 32)) {
-    const int Nx = a.Nx, x = t.x0 + t.lane;
-    double *orow = a.dst + ((int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) + (ybase - a.out_y0)) * Nx + x;
-    if (full) {
-#pragma unroll
-      for (int j = 0; j < R; ++j) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < R; ++j)
-        if (x < Nx && ybase + j < a.out_y1) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
-  GDM_STAMPT(t, zz - t.zs, 4);
-}
-
-template <int JP, int P, int R, int NC, int NP, int BK, int PF, bool WALL, bool YW>
-__device__ __forceinline__ void cblock8(const StencilArgs &a, const Tile7 &t, int ybase, bool full,
-                                        double (&acc)[2 * P + 1][R], int zb) {
-  if constexpr (JP < 2 * P + 1) {
-    cplane8<JP, P, R, NC, NP, BK, PF, WALL, YW>(a, t, ybase, full, acc, zb + JP);
-    cblock8<JP + 1, P, R, NC, NP, BK, PF, WALL, YW>(a, t, ybase, full, acc, zb);
-  }
-}
-
-template <int P, int R, int NC, int NP, int BK, int PF, bool ZI, bool YW>
-__device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7 &t, int ybase, bool full) {
-  using G = Geom8<P, R, NC, NP, BK>;
-  constexpr int W = G::W;
-  double acc[W][R];
-#pragma unroll
-  for (int s = 0; s < W; ++s)
-#pragma unroll
-    for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
-  GDM_LDS_BARRIER();  // tables in LDS
-  // ZI: the host launched this kernel only on output planes whose z columns
-  // are all interior -> compile-time z bands, no table reads; otherwise every
-  // plane reads its column (wall columns or the interior one) from LDS
-  // (one launch for all planes, choosing the compile-time or the table z
-  // column per block of W planes, measured 1.25 vs 0.86 ms at C3: the
-  // consumer loop carries both paths; profiles/r3j/ab_zmix.txt)
-  for (int zb = t.zs; zb < t.zend; zb += W)
-    cblock8<0, P, R, NC, NP, BK, PF, !ZI, YW>(a, t, ybase, full, acc, zb);
-}
-
-template <int P, int R, int NC, int NP, int BK, int PF, bool ZI>
-__device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) {
-  using G = Geom8<P, R, NC, NP, BK>;
-  const int ybase = t.y0 + t.cw * R;
-  const bool full = (t.x0 + G::TX <= a.Nx) && (ybase + R <= a.out_y1);
-  // edge tiles (rows next to a y wall) wait for the producers' y-wall
-  // corrections every plane: their own copy of the loop keeps that out of the
-  // hot block of the other tiles
-  if (t.yedge)
-    consumer8_loop<P, R, NC, NP, BK, PF, ZI, true>(a, t, ybase, full);
-  else
-    consumer8_loop<P, R, NC, NP, BK, PF, ZI, false>(a, t, ybase, full);
-}
-
-template <int P, int R, int NC, int NP, int BK, int CH, int PF, bool ZI>
-__global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, NP, BK>::WGS) / 4)
-    stencil8_kernel(StencilArgs a) {
-  using G = Geom8<P, R, NC, NP, BK>;
-  static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget of one workgroup per CU");
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  ldouble *lds = (ldouble *)smem;
-  Tile7 t;
-  t.u0 = lds;
-  t.ab0 = lds + G::OFF_AB;
-  t.zt = lds + G::OFF_ZT;
-  t.yc = lds + G::OFF_YC;
-  t.corr = lds + G::OFF_CORR;
-  t.yw = lds + G::OFF_YW;
-  t.lane = threadIdx.x & 63;
-  t.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  t.cw = t.wv - NP;
-  // XCD-aware tile order: the hardware deals workgroup b to XCD b % 8; XCD k
-  // gets the contiguous logical range [k q, (k + 1) q) of tiles (x fastest),
-  // so the tiles sharing x- and y-halo lines run on one XCD at the same time
-  // and those lines are fetched from HBM once into that XCD's L2.
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (a.xcd_map) {
-    const int64_t gx = gridDim.x, gy = gridDim.y;
-    const int64_t nb = gx * gy * gridDim.z, q = nb / 8;
-    const int64_t b = blockIdx.x + gx * (blockIdx.y + gy * (int64_t)blockIdx.z);
-    const int64_t L = b >= 8 * q ? b : (b % 8) * q + b / 8;
-    bx = (int)(L % gx);
-    by = (int)((L / gx) % gy);
-    bz = (int)(L / (gx * gy));
-  }
-  t.sid = bx + gridDim.x * (by + gridDim.y * bz);
-  t.x0 = bx * G::TX;
-  t.y0 = a.out_y0 + by * G::TY;
-#ifdef GDM_EXP_NOY
-  t.yedge = false;  // timing experiment: wrong next to the y walls
-#else
-  t.yedge = ywall_begin<P, G::TY>(a, t.y0) >= 0;
-#endif
-  {
-    const int r = bz < a.nchunk0 ? 0 : 1;
-    const int c = bz - (r ? a.nchunk0 : 0);
-    t.zc0 = a.cz0[r] + c * a.zchunk;
-    t.zc1 = min(t.zc0 + a.zchunk, a.cz1[r]);
-  }
-  t.zs = max(t.zc0 - P, a.in_z0);
-  t.ze = min(t.zc1 + P, a.in_z1);
-  t.zend = t.zc1 + P;
-  {
-    const int L = a.x_corr_left, rb = a.Nx - a.x_corr_right;
-    t.nl = max(0, min(L, t.x0 + G::TX) - t.x0);
-    t.rs = max(rb, t.x0);
-    const int nr = max(0, min(a.Nx, t.x0 + G::TX) - t.rs);
-    t.ncw = t.nl + nr;
-#ifdef GDM_EXP_NOX
-    t.ncw = 0;  // timing experiment: wrong next to the x walls
-#endif
-  }
-  if (!ZI)
-    for (int e = threadIdx.x; e < G::ZTSZ; e += G::NT) t.zt[e] = a.zt[e];
-  if (t.ncw > 0)
-    for (int e = threadIdx.x; e < G::CORRSZ; e += G::NT) t.corr[e] = a.corrX[e];
-  // tiles with rows next to a y wall: (wall - Toeplitz) column corrections
-  if (t.yedge)
-    for (int e = threadIdx.x; e < G::UR * G::W; e += G::NT) {
-      const int r = e / G::W, k = e - r * G::W;
-      t.yc[2 * e] = a.yT1[(size_t)(t.y0 + r) * G::W + k];
-      t.yc[2 * e + 1] = a.yT3[(size_t)(t.y0 + r) * G::W + k];
-    }
-#if defined(GDM_EXP_ONLYCONS)
-  if (t.wv >= NP) consumer8<P, R, NC, NP, BK, PF, ZI>(a, t);
-#elif defined(GDM_EXP_ONLYPROD)
-  if (t.wv < NP) producer8<P, R, NC, NP, BK, CH>(a, t);
-#else
-  if (t.wv < NP)
-    producer8<P, R, NC, NP, BK, CH>(a, t);
-  else
-    consumer8<P, R, NC, NP, BK, PF, ZI>(a, t);
-#endif
-}
-
-// ===========================================================================
-// Fused Kronecker stencil, v9: every wave plays both roles.
-//
-// s_memtime stamps of v8 (tools/stamp_stencil.py, profiles/r4b) showed its
-// producer waves parked at the plane barrier for ~60 % of every plane while
-// the consumers' y/z FMA chains set the period.  Here all NW = 16 waves own R
-// = 2 output rows (the z ring is 2p+1 planes x 2 rows, so it fits beside the
-// x-sweep's registers) and the first NG waves also run the x-sweep of one
-// 4-row group: every SIMD keeps four waves with work, and the x-sweep's
-// independent FMAs fill the latency of the y/z chains.  One barrier per plane:
-//   B_i | Y(i) (+ own y-wall rows) | Z(i) | retire | [w < NG] X(i+1) -> AB (i+1)&1, DMA(i+3)
-// X(i+1) overwrites the AB buffer that every wave read in Y(i-1), before B_i.
-// Output rows are written with buffer stores (out-of-range lanes dropped by
-// the resource's bound), so every retire issues exactly R stores and the
-// counted vmcnt before X(i+1) stays exact.
-// ===========================================================================
-#ifndef GDM_V9_XF
-#define GDM_V9_XF 1
-#endif
-template <int P, int R, int NW, int BK>
-using Geom9 = Geom8<P, R, NW, NW, BK>;
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-// wait until the DMA of the plane the next x-sweep reads has landed: the
-// VMEM instructions issued after it are the `stores` buffer stores since then
-// plus, if next_dma, the DMA of the following plane (nd instructions)
-template <int N, int R>
-__device__ __forceinline__ void wait_vm9(int stores) {
-  if (stores <= 0) GDM_WAIT_VMCNT(N);
-  else if (stores <= R) GDM_WAIT_VMCNT(N + R);
-  else if (stores <= 2 * R) GDM_WAIT_VMCNT(N + 2 * R);
-  else if (stores <= 3 * R) GDM_WAIT_VMCNT(N + 3 * R);
-  else GDM_WAIT_VMCNT(N + 4 * R);
-}
-
-template <int I, int P, int R, int NW, int BK, int CH>
-__device__ __forceinline__ void wait_dma9(int wv, bool next_dma, int stores) {
-  if constexpr (I < NW) {
-    if (wv == I) {
-      if (next_dma)
-        wait_vm9<Dma7<P, R, NW, NW, BK, CH>::nd(I), R>(stores);
-      else
-        wait_vm9<0, R>(stores);
-      return;
-    }
-    wait_dma9<I + 1, P, R, NW, BK, CH>(wv, next_dma, stores);
-  }
-}
-
-// x-sweep of this wave's row group g = wv of the plane in u slot `us` into
-// the AB buffer `ab` (+ x-wall corrections on wall tiles)
-template <int P, int R, int NW, int BK>
-__device__ __forceinline__ void xstep9(const StencilArgs &a, const Tile7 &t, lcdouble *us, ldouble *ab,
-                                       const XWallPre<P, BK> &xpre) {
-  Tile7 tt = t;
-  tt.ab0 = ab;
-  dpair V[4];
-  xsweep8<P, R, NW, NW, BK>(a, tt, us, t.wv, V);
-  write_ab8<P, R, NW, NW, BK>(tt, t.wv, V);
-  if (t.ncw > 0) {
-    XWall<P, BK> xw;
-    xwall8_calc<P, R, NW, NW, BK>(tt, us, t.wv, xpre, xw);
-    xwall8_add<P, BK>(tt, xw);
-  }
-}
-
-// y-wall rows of this wave (edge tiles): D += sum_s c1(y, s) A(s), E += sum_s
-// c1 B(s) + c3 A(s) with the (wall - Toeplitz) column tables (cf. ywall8)
-template <int P, int R, int NW, int BK>
-__device__ __forceinline__ void ywall9(const StencilArgs &a, const Tile7 &t, int ybase, double (&D)[R],
-                                       double (&E)[R]) {
-  using G = Geom9<P, R, NW, BK>;
-  constexpr int W = G::W, TX = G::TX;
-  const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int y = ybase + j;
-    if (y >= yb && y < ye) {
-      double dD = 0.0, dE = 0.0;
-#pragma unroll 1
-      for (int k = 0; k < W; ++k) {
-        const int rs = y + 2 * P - k - t.y0;
-        const dpair c = ((lcdouble2 *)t.yc)[rs * W + k];
-        if constexpr (BK != 0) {
-          const dpair v = *(lcdouble2 *)(t.ab0 + G::ab(rs, t.lane));
-          dD = fma(c.x, v.x, dD);
-          dE = fma(c.x, v.y, fma(c.y, v.x, dE));
-        } else {
-          dD = fma(c.x, t.ab0[rs * TX + t.lane], dD);
-        }
-      }
-      D[j] += dD;
-      E[j] += dE;
-    }
-  }
-}
-
-template <int P, int R, int NW, int BK, int CH>
-struct Pipe9 {
-  ldouble *u[2];
-  DmaPre7<P, R, NW, NW, BK, CH> dpre;
-  XWallPre<P, BK> xpre;
-  int ybase;
-  uint32_t ocol;  // this lane's byte column x * 8, or out of range
-  // buffer stores issued between the last two DMA issues (st0) and since the
-  // last one (st1): the counted vmcnt before an x-sweep
-  int st0, st1;
-};
-
-template <int P, int R, int NW, int BK, int CH>
-__device__ __forceinline__ void dma9(const StencilArgs &a, const Tile7 &t, int zz, const Pipe9<P, R, NW, BK, CH> &pp,
-                                     int slot) {
-#if defined(__HIP_DEVICE_COMPILE__)  // (clang's host pass rejects this instantiation; device code only)
-  stage_plane_pre7<P, R, NW, NW, BK, CH>(a, t, zz, pp.u[slot], pp.dpre);
-#endif
-}
-
-template <int P, int R, int NW, int BK, int CH>
-__device__ __forceinline__ void dma9c(const StencilArgs &a, const Tile7 &t, int zz, Pipe9<P, R, NW, BK, CH> &pp,
-                                      int slot) {
-  dma9<P, R, NW, BK, CH>(a, t, zz, pp, slot);
-  pp.st0 = pp.st1;
-  pp.st1 = 0;
-}
-
-// X(i + 1) of plane zz + 1 into AB buffer (i + 1) & 1, then DMA(i + 3) into the
-// u slot it read (waves < NG)
-template <int P, int R, int NW, int BK, int CH>
-__device__ __forceinline__ void xpart9(const StencilArgs &a, const Tile7 &t, Pipe9<P, R, NW, BK, CH> &pp, int zz) {
-  using G = Geom9<P, R, NW, BK>;
-  const int i = zz - t.zs;
-  if (zz + 1 < t.ze && t.wv < G::NG) {
-    const bool next = zz + 2 < t.ze;
-    wait_dma9<0, P, R, NW, BK, CH>(t.wv, next, next ? pp.st0 + pp.st1 : pp.st1);
-    const int s1 = (i + 1) & 1;
-    xstep9<P, R, NW, BK>(a, t, pp.u[s1], t.ab0 + s1 * G::ABSZ, pp.xpre);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (zz + 3 < t.ze) dma9c<P, R, NW, BK, CH>(a, t, zz + 3, pp, s1);
-  }
-}
-
-// stores of output plane zz - p happen in interval zz - zs when the plane is
-// in this chunk's output range
-__device__ __forceinline__ bool retires9(const Tile7 &t, int zz, int P) {
-  const int zo = zz - P;
-  return zo >= t.zc0 && zo < t.zc1;
-}
-
-template <int JP, int P, int R, int NW, int BK, int CH, int PF, bool WALL, bool YW, bool XF>
-__device__ __forceinline__ void cplane9(const StencilArgs &a, const Tile7 &t, Pipe9<P, R, NW, BK, CH> &pp,
-                                        double (&acc)[2 * P + 1][R], int zz) {
-  using G = Geom9<P, R, NW, BK>;
-  using IR = InteriorRows<P>;
-  constexpr int W = G::W;
-  const int i = zz - t.zs;
-  if (zz < t.ze) {
-    double D[R], E[R];
-    GDM_STAMPT(t, i, 0);
-    GDM_LDS_BARRIER();  // B_i: AB(i) complete
-    GDM_STAMPT(t, i, 1);
-    if constexpr (XF) xpart9<P, R, NW, BK, CH>(a, t, pp, zz);
-    Tile7 tt = t;
-    tt.ab0 = t.ab0 + (i & 1) * G::ABSZ;
-    ysweep8<P, R, NW, NW, BK, PF>(a, tt, D, E);
-    if constexpr (YW) ywall9<P, R, NW, BK>(a, tt, pp.ybase, D, E);
-    GDM_STAMPT(t, i, 2);
+    sync_signal(t.sync + SY_FREE + bs);
     if constexpr (!WALL) {
+      // interior z column: out += mhat[k] E + zd[k] D with zd = dint dhat[2p - k]
+      // (the scale folded into the coefficients; zd[p] = 0 for advection)
 #pragma unroll
       for (int k = 0; k < W; ++k) {
         GDM_FENCE();
@@ -1507,6 +1086,7 @@ __device__ __forceinline__ void cplane9(const StencilArgs &a, const Tile7 &t, Pi
         }
       }
     } else {
+      // wall blocks: every plane from the column table (row 2W = interior)
       const int row = zz < W ? zz : (zz >= a.Nz - W ? W + zz - (a.Nz - W) : 2 * W);
       lcdouble2 *zc = (lcdouble2 *)t.zt + row * W;
       dpair cur = zc[0];
@@ -1526,64 +1106,84 @@ __device__ __forceinline__ void cplane9(const StencilArgs &a, const Tile7 &t, Pi
       }
     }
   }
-  GDM_STAMPT(t, i, 3);
+  // The ring values only feed the conditional retire stores; without this
+  // opaque use LLVM sinks each slot's whole FMA chain into its store branch
+  // and keeps every plane's D/E and coefficients alive until then.
 #pragma unroll
   for (int s = 0; s < W; ++s)
 #pragma unroll
     for (int j = 0; j < R; ++j) asm volatile("" : "+v"(acc[s][j]));
-  // retire output plane zz - p: R buffer stores (lanes out of the box dropped)
+  // retire output plane zz - p
   constexpr int rslot = (JP - P + 2 * W) % W;
-  if (retires9(t, zz, P)) {
-    const int zo = zz - P;
-    const int ny_out = a.out_y1 - a.out_y0;
-    const double *plane = a.dst + (int64_t)(zo - a.out_z0) * ny_out * a.Nx;
-    __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)plane, 0, (int)((int64_t)ny_out * a.Nx * 8), 0x00020000);
+  const int zo = zz - P;
+  if (zo >= t.zc0 && zo < t.zc1) {
+    const int Nx = a.Nx, x = t.x0 + t.lane;
+    double *orow = a.dst + ((int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) + (ybase - a.out_y0)) * Nx + x;
+    if (full) {
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int yr = pp.ybase + j;
-      const uint32_t off = (yr < a.out_y1 && pp.ocol != 0x80000000u)
-                               ? (uint32_t)((yr - a.out_y0) * a.Nx * 8) + pp.ocol
-                               : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc[rslot][j]), rs, off, 0,
-                                            GDM_STENCIL_ST_NT ? 2 : 0);
+      for (int j = 0; j < R; ++j) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (x < Nx && ybase + j < a.out_y1) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
     }
-    pp.st1 += R;
   }
 #pragma unroll
   for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
-  GDM_STAMPT(t, i, 4);
-  if constexpr (!XF) xpart9<P, R, NW, BK, CH>(a, t, pp, zz);
-  GDM_STAMPT(t, i, 5);
 }
 
-template <int JP, int P, int R, int NW, int BK, int CH, int PF, bool WALL, bool YW, bool XF>
-__device__ __forceinline__ void cblock9(const StencilArgs &a, const Tile7 &t, Pipe9<P, R, NW, BK, CH> &pp,
+template <int JP, int P, int R, int NC, int NP, int BK, int PF, bool WALL, bool YW>
+__device__ __forceinline__ void cblock8(const StencilArgs &a, const Tile7 &t, int ybase, bool full, bool ywave,
                                         double (&acc)[2 * P + 1][R], int zb) {
   if constexpr (JP < 2 * P + 1) {
-    cplane9<JP, P, R, NW, BK, CH, PF, WALL, YW, XF>(a, t, pp, acc, zb + JP);
-    cblock9<JP + 1, P, R, NW, BK, CH, PF, WALL, YW, XF>(a, t, pp, acc, zb);
+    cplane8<JP, P, R, NC, NP, BK, PF, WALL, YW>(a, t, ybase, full, ywave, acc, zb + JP);
+    cblock8<JP + 1, P, R, NC, NP, BK, PF, WALL, YW>(a, t, ybase, full, ywave, acc, zb);
   }
 }
 
-template <int P, int R, int NW, int BK, int CH, int PF, bool ZI, bool YW, bool XF>
-__device__ __forceinline__ void loop9(const StencilArgs &a, const Tile7 &t, Pipe9<P, R, NW, BK, CH> &pp) {
-  using G = Geom9<P, R, NW, BK>;
+template <int P, int R, int NC, int NP, int BK, int PF, bool ZI, bool YW>
+__device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7 &t, int ybase, bool full,
+                                               bool ywave) {
+  using G = Geom8<P, R, NC, NP, BK>;
   constexpr int W = G::W;
   double acc[W][R];
 #pragma unroll
   for (int s = 0; s < W; ++s)
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
-  for (int zb = t.zs; zb < t.zend; zb += W) cblock9<0, P, R, NW, BK, CH, PF, !ZI, YW, XF>(a, t, pp, acc, zb);
+  GDM_LDS_BARRIER();  // tables in LDS, counters zeroed
+  // ZI: the host launched this kernel only on output planes whose z columns
+  // are all interior -> compile-time z bands, no table reads; otherwise every
+  // plane reads its column (wall columns or the interior one) from LDS
+  // (one launch for all planes, choosing the compile-time or the table z
+  // column per block of W planes, measured 1.25 vs 0.86 ms at C3: the
+  // consumer loop carries both paths; profiles/r3j/ab_zmix.txt)
+  for (int zb = t.zs; zb < t.zend; zb += W)
+    cblock8<0, P, R, NC, NP, BK, PF, !ZI, YW>(a, t, ybase, full, ywave, acc, zb);
 }
 
-template <int P, int R, int NW, int BK, int CH, int PF, bool ZI>
-__global__ void __launch_bounds__(64 * NW, NW / 4) stencil9_kernel(StencilArgs a) {
-  using G = Geom9<P, R, NW, BK>;
-  static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget of one workgroup per CU");
-  static_assert(G::NPASS == 1, "one x-sweep row group per wave");
-  constexpr int NT = 64 * NW;
+template <int P, int R, int NC, int NP, int BK, int PF, bool ZI>
+__device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  const int ybase = t.y0 + t.cw * R;
+  const bool full = (t.x0 + G::TX <= a.Nx) && (ybase + R <= a.out_y1);
+  // edge tiles (rows next to a y wall) wait for the producers' y-wall
+  // corrections every plane: their own copy of the loop keeps that out of the
+  // hot block of the other tiles
+  if (t.yedge) {
+    const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
+    const bool ywave = ybase < ye && ybase + R > yb;
+    consumer8_loop<P, R, NC, NP, BK, PF, ZI, true>(a, t, ybase, full, ywave);
+  } else {
+    consumer8_loop<P, R, NC, NP, BK, PF, ZI, false>(a, t, ybase, full, false);
+  }
+}
+
+template <int P, int R, int NC, int NP, int BK, int CH, int PF, bool ZI>
+__global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, NP, BK>::WGS) / 4)
+    stencil8_kernel(StencilArgs a) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  static_assert(G::lds_bytes() <= G::LDS_CAP, "LDS budget");
   extern __shared__ __attribute__((aligned(16))) double smem[];
   ldouble *lds = (ldouble *)smem;
   Tile7 t;
@@ -1592,10 +1192,15 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) stencil9_kernel(StencilArgs a
   t.zt = lds + G::OFF_ZT;
   t.yc = lds + G::OFF_YC;
   t.corr = lds + G::OFF_CORR;
+  t.sync = (lu32 *)(lds + G::OFF_SYNC);
   t.yw = lds + G::OFF_YW;
   t.lane = threadIdx.x & 63;
   t.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  t.cw = t.wv;
+  t.cw = t.wv - NP;
+  // XCD-aware tile order: the hardware deals workgroup b to XCD b % 8; XCD k
+  // gets the contiguous logical range [k q, (k + 1) q) of tiles (x fastest),
+  // so the tiles sharing x- and y-halo lines run on one XCD at the same time
+  // and those lines are fetched from HBM once into that XCD's L2.
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (a.xcd_map) {
     const int64_t gx = gridDim.x, gy = gridDim.y;
@@ -1606,10 +1211,11 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) stencil9_kernel(StencilArgs a
     by = (int)((L / gx) % gy);
     bz = (int)(L / (gx * gy));
   }
-  t.sid = bx + gridDim.x * (by + gridDim.y * bz);
   t.x0 = bx * G::TX;
   t.y0 = a.out_y0 + by * G::TY;
-  t.yedge = ywall_begin<P, G::TY>(a, t.y0) >= 0;
+  const int yb = ywall_begin<P, G::TY>(a, t.y0);
+  t.yedge = yb >= 0;
+  t.ry0 = yb - t.y0;
   {
     const int r = bz < a.nchunk0 ? 0 : 1;
     const int c = bz - (r ? a.nchunk0 : 0);
@@ -1626,54 +1232,25 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) stencil9_kernel(StencilArgs a
     const int nr = max(0, min(a.Nx, t.x0 + G::TX) - t.rs);
     t.ncw = t.nl + nr;
   }
+  if (threadIdx.x < G::NSYNC) t.sync[threadIdx.x] = 0u;
   if (!ZI)
-    for (int e = threadIdx.x; e < G::ZTSZ; e += NT) t.zt[e] = a.zt[e];
+    for (int e = threadIdx.x; e < G::ZTSZ; e += G::NT) t.zt[e] = a.zt[e];
   if (t.ncw > 0)
-    for (int e = threadIdx.x; e < G::CORRSZ; e += NT) t.corr[e] = a.corrX[e];
-  if (t.yedge)
-    for (int e = threadIdx.x; e < G::UR * G::W; e += NT) {
-      const int r = e / G::W, k = e - r * G::W;
-      t.yc[2 * e] = a.yT1[(size_t)(t.y0 + r) * G::W + k];
-      t.yc[2 * e + 1] = a.yT3[(size_t)(t.y0 + r) * G::W + k];
-    }
-  Pipe9<P, R, NW, BK, CH> pp;
-  pp.u[0] = t.u0;
-  pp.u[1] = t.u0 + G::USZ;
-  pp.ybase = t.y0 + t.cw * R;
-  {
-    const int x = t.x0 + t.lane;
-    pp.ocol = x < a.Nx ? (uint32_t)x * 8u : 0x80000000u;
-  }
-  pp.st0 = pp.st1 = 0;
-  const int n = t.ze - t.zs;
-  if (t.wv < G::NG) {
-    stage_pre7<P, R, NW, NW, BK, CH>(a, t, pp.dpre);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (k < n) dma9c<P, R, NW, BK, CH>(a, t, t.zs + k, pp, k);
-    if (t.ncw > 0) xwall8_pre<P, R, NW, NW, BK>(a, t, pp.xpre);
-  }
-  GDM_LDS_BARRIER();  // tables in LDS
-  if (t.wv < G::NG && n > 0) {
-    wait_dma9<0, P, R, NW, BK, CH>(t.wv, n > 1, 0);
-    xstep9<P, R, NW, BK>(a, t, pp.u[0], t.ab0, pp.xpre);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (n > 2) dma9c<P, R, NW, BK, CH>(a, t, t.zs + 2, pp, 0);
-  }
-  // odd x-sweep waves run X(i+1) before their y/z work, so every SIMD holds
-  // waves in both phases (GDM_V9_XF=0: all after)
-  const bool xf = GDM_V9_XF && (t.wv & 1) && t.wv < G::NG;
+    for (int e = threadIdx.x; e < G::CORRSZ; e += G::NT) t.corr[e] = a.corrX[e];
+  // y-wall tiles: (wall - Toeplitz) column corrections of the tile rows
+  // [ry0, ry0 + YCR) (global table row = y0 + tile row; tables are padded by p)
   if (t.yedge) {
-    if (xf)
-      loop9<P, R, NW, BK, CH, PF, ZI, true, true>(a, t, pp);
-    else
-      loop9<P, R, NW, BK, CH, PF, ZI, true, false>(a, t, pp);
-  } else {
-    if (xf)
-      loop9<P, R, NW, BK, CH, PF, ZI, false, true>(a, t, pp);
-    else
-      loop9<P, R, NW, BK, CH, PF, ZI, false, false>(a, t, pp);
+    const int nr = min(G::YCR, G::UR - t.ry0);
+    for (int e = threadIdx.x; e < nr * G::W; e += G::NT) {
+      const int r = e / G::W, k = e - r * G::W;
+      t.yc[2 * e] = a.yT1[(size_t)(t.y0 + t.ry0 + r) * G::W + k];
+      t.yc[2 * e + 1] = a.yT3[(size_t)(t.y0 + t.ry0 + r) * G::W + k];
+    }
   }
+  if (t.wv < NP)
+    producer8<P, R, NC, NP, BK, CH>(a, t);
+  else
+    consumer8<P, R, NC, NP, BK, PF, ZI>(a, t);
 }
 
 // ---------------------------------------------------------------------------
@@ -2092,44 +1669,6 @@ static hipError_t launch8_z(int bk, const StencilArgs &a, hipStream_t st) {
   }
 }
 
-template <int P, int R, int NW, int BK, int CH, int PF, bool ZI>
-static hipError_t launch9_t(const StencilArgs &a, hipStream_t st) {
-  using G = Geom9<P, R, NW, BK>;
-  const size_t lds = G::lds_bytes();
-  {
-    static std::atomic<uint64_t> attr_mask{0};
-    hipError_t e = gdmk_set_lds_attr((const void *)stencil9_kernel<P, R, NW, BK, CH, PF, ZI>, lds, attr_mask);
-    if (e != hipSuccess) return e;
-  }
-  int nz = 0;
-  for (int r = 0; r < 2; ++r)
-    if (a.cz1[r] > a.cz0[r]) nz += (a.cz1[r] - a.cz0[r] + a.zchunk - 1) / a.zchunk;
-  dim3 grid((a.Nx + G::TX - 1) / G::TX, (a.out_y1 - a.out_y0 + G::TY - 1) / G::TY, nz);
-  if (grid.x == 0 || grid.y == 0 || grid.z == 0) return hipSuccess;
-  hipLaunchKernelGGL((stencil9_kernel<P, R, NW, BK, CH, PF, ZI>), grid, dim3(64 * NW), lds, st, a);
-  return hipGetLastError();
-}
-
-template <int P, int R, int NW, int PF, bool ZI>
-static hipError_t launch9_z(int bk, const StencilArgs &a, hipStream_t st) {
-  const bool vec = (a.Nx % 2 == 0) && ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0);
-  switch (bk) {
-#ifdef GDM_ONLY_ADV16
-    case 1: return vec ? launch9_t<P, R, NW, 1, 16, PF, ZI>(a, st) : hipErrorInvalidValue;
-#else
-    case 0: return vec ? launch9_t<P, R, NW, 0, 16, PF, ZI>(a, st) : launch9_t<P, R, NW, 0, 4, PF, ZI>(a, st);
-    case 1: return vec ? launch9_t<P, R, NW, 1, 16, PF, ZI>(a, st) : launch9_t<P, R, NW, 1, 4, PF, ZI>(a, st);
-    case 2: return vec ? launch9_t<P, R, NW, 2, 16, PF, ZI>(a, st) : launch9_t<P, R, NW, 2, 4, PF, ZI>(a, st);
-#endif
-    default: return hipErrorInvalidValue;
-  }
-}
-
-template <int P, int R, int NW, int PF>
-static hipError_t launch9_p(int bk, bool zint, const StencilArgs &a, hipStream_t st) {
-  return zint ? launch9_z<P, R, NW, PF, true>(bk, a, st) : launch9_z<P, R, NW, PF, false>(bk, a, st);
-}
-
 template <int P, int R, int NC, int NP, int PF>
 static hipError_t launch8_p(int bk, bool zint, const StencilArgs &a, hipStream_t st) {
   return zint ? launch8_z<P, R, NC, NP, PF, true>(bk, a, st) : launch8_z<P, R, NC, NP, PF, false>(bk, a, st);
@@ -2147,11 +1686,7 @@ extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, bool zint, const gdmk:
     case 3: return launch8_p<3, 4, 8, 8, 3>(bk, zint, a, st);
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 5
-#ifdef GDM_V9_P5
-    case 5: return launch9_p<5, 2, 16, GDM_V9_P5>(bk, zint, a, st);
-#else
     case 5: return launch8_p<5, GDM_R5, GDM_NC5, GDM_NP5, GDM_PF5>(bk, zint, a, st);
-#endif
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 7
     case 7: return launch8_p<7, GDM_R7, GDM_NC7, GDM_NP7, GDM_PF7>(bk, zint, a, st);

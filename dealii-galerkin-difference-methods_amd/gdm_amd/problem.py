@@ -122,17 +122,27 @@ class AdvectionProblem:
         if op.mesh.n_ranks != 1:
             raise GdmError("AdvectionProblem: single-rank driver")
         self.op, self.fn, self.prm = op, int(fn_kind), list(fn_params)
-        self.carry_bc = bool(carry_bc)  # False: self.bc is not maintained
-        nb = max(op.n_bc_points, 1)
+        self.carry_bc = bool(carry_bc)
         import torch
 
         dev = "cuda:%d" % op.device
-        z = lambda m: torch.zeros(m, dtype=torch.float64, device=dev)  # noqa: E731
+        # block(0) (the boundary points, ~28 M at C3) exists only on the explicit
+        # path: with carry_bc=False the engine computes the stage values itself
+        nb = max(op.n_bc_points, 1) if self.carry_bc else 0
+        z = lambda m: torch.zeros(m, dtype=torch.float64, device=dev) if m else None  # noqa: E731
         self.u = op.new_vector(False)
-        self.bc = z(nb)
+        self._bc = z(nb)
         self._acc = [z(nb), op.new_vector(False)]
         self._Y = [z(nb), op.new_vector(False)]
         self._k = [z(nb), op.new_vector(False)]
+
+    @property
+    def bc(self):
+        """block(0) = g at the boundary points; kept only with carry_bc=True"""
+        if not self.carry_bc:
+            raise GdmError("AdvectionProblem.bc: block(0) is not kept (carry_bc=False computes the stage "
+                           "boundary values on the device)")
+        return self._bc
 
     def initialize_time_step(self, t):
         """block(0) = g(t_n) at the boundary points (stiffness.h:181-194)"""

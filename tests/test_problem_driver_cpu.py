@@ -118,3 +118,16 @@ def test_wave_stage_order(no_torch):
         assert src is (pr.u if s == 0 else pr._Y[0])
         _, args, _ = op.calls[3 * s + 1]
         assert args[1] is (pr.v if s == 0 else pr._Y[1])  # ku = stage v, before it is overwritten
+
+
+def test_advection_no_block0_vectors_without_carry_bc(no_torch):
+    """with the engine computing the stage boundary values, no
+    block(0) vector is allocated (28 M points at C3) and .bc refuses"""
+    from gdm_amd._capi import GdmError
+
+    pr = AdvectionProblem(_Op(), 2, [0.0] * 9)
+    assert pr._acc[0] is None and pr._Y[0] is None and pr._k[0] is None
+    with pytest.raises(GdmError):
+        pr.bc
+    pr2 = AdvectionProblem(_Op(), 2, [0.0] * 9, carry_bc=True)
+    assert pr2.bc is not None and pr2._acc[0] is not None

@@ -2,7 +2,7 @@
 NAME=$1; shift
 C=/root/repo/dealii-galerkin-difference-methods_amd/csrc
 B=/root/repo/dealii-galerkin-difference-methods_amd/lib/obj
-O=/root/repo/dealii-galerkin-difference-methods_amd/lib/variants/$NAME
+O=/root/repo/dealii-galerkin-difference-methods_amd/lib/ab/$NAME
 mkdir -p $O
 F="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -Wno-unused-function $*"
 /opt/rocm/bin/hipcc $F -c $C/gdm_mass.hip -o $O/mass.o &&

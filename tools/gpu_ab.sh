@@ -6,7 +6,7 @@
 export TMPDIR=/tmp
 TAG=$1; CFG=$2; KIND=$3; shift 3
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
-V=dealii-galerkin-difference-methods_amd/lib/variants
+V=dealii-galerkin-difference-methods_amd/lib/ab
 for rep in 1 2; do
   for L in "$@"; do
     if [ "$L" = main ]; then unset GDM_HIP_LIB; else export GDM_HIP_LIB=$V/$L/libgdm_hip.so; fi

@@ -4,7 +4,7 @@
 export TMPDIR=/tmp; TAG=$1; shift; O=gpurun_out/$TAG; mkdir -p $O
 for rep in 1 2; do
   for L in "$@"; do
-    if [ $L = main ]; then unset GDM_HIP_LIB; else export GDM_HIP_LIB=dealii-galerkin-difference-methods_amd/lib/variants/$L/libgdm_hip.so; fi
+    if [ $L = main ]; then unset GDM_HIP_LIB; else export GDM_HIP_LIB=dealii-galerkin-difference-methods_amd/lib/ab/$L/libgdm_hip.so; fi
     timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/$L$rep -o ks --output-format csv -- python -u tools/bench_ops.py --configs C3,C4 --ops mass_solve --iters 10 > $O/$L$rep.log 2>&1 || exit 1
     find $O/$L$rep -name "*kernel_stats.csv" -exec cp {} $O/ks_$L$rep.csv \;
     python3 -c "

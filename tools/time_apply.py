@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Timing only (no parity) of compute_rhs without inflow data at C3 for the
-libraries given as arguments (variant names under lib/variants, "main" = the
+libraries given as arguments (variant names under lib/ab, "main" = the
 in-tree build), each in a child process.  Experiment tool for builds whose
 results are wrong by design (phase-disable / role-only experiments).
 
@@ -12,7 +12,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-V = os.path.join(ROOT, "dealii-galerkin-difference-methods_amd", "lib", "variants")
+V = os.path.join(ROOT, "dealii-galerkin-difference-methods_amd", "lib", "ab")
 CHILD = r'''
 import sys, torch
 sys.path.insert(0, %r)
