@@ -73,8 +73,7 @@ struct Face {
   int64_t n_points = 0;
   FaceDir t0, t1;
   int64_t base = 0;       // owned index of node (i0 = 0, i1 = t1.node_begin)
-  double *T = nullptr;    // step-1 scratch of this face (faces run concurrently)
-  double *G = nullptr;    // step-2 result of this face (node-major [i1][i0]), added after the join
+  double *T = nullptr;    // step-1 result of this face (faces run concurrently)
 };
 
 }  // namespace
@@ -648,10 +647,6 @@ void build_faces(gdm_op *op) {
       const int64_t tsz = std::max<int64_t>(1, (int64_t)F.t1.Q * (F.t0.node_end - F.t0.node_begin));
       hip_check(hipMalloc(&F.T, sizeof(double) * tsz), "hipMalloc");
       keep(op, F.T);
-      const int64_t gsz = std::max<int64_t>(1, (int64_t)(F.t0.node_end - F.t0.node_begin) *
-                                                   (F.t1.node_end - F.t1.node_begin));
-      hip_check(hipMalloc(&F.G, sizeof(double) * gsz), "hipMalloc");
-      keep(op, F.G);
     }
     op->faces.push_back(F);
   }
@@ -681,8 +676,7 @@ void build_faces(gdm_op *op) {
 
 // Output planes [zb, ze) of the owned range (3D: z planes; the full owned
 // range otherwise).  dst is the owned vector; only those planes are written.
-hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst, int zb = -1, int ze = -1,
-                          hipStream_t wall_stream = nullptr) {
+hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst, int zb = -1, int ze = -1) {
   const gdm_layout &L = op->layout;
   gdmk::StencilArgs a{};
   a.src = src;
@@ -748,59 +742,39 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
     a.out_z1 = ze;
     return gdmk_launch_stencil(op->p, bk, a, op->stream);
   }
-  // v8: output planes whose z columns are all interior (z' in [3p+1, Nz-3p-2])
-  // go to the compile-time-band kernel; the rest (next to the z walls) to the
-  // table kernel, both ranges of it in one launch.
-  const int p = op->p, zlo = 3 * p + 1, zhi = a.Nz - 3 * p - 1;
-  const int i0 = std::max(zb, zlo), i1 = std::min(ze, zhi);
-  // every plane in [zlo, zhi) goes to the compile-time-band kernel, whatever
-  // the launched range: the table rows of the interior column round
-  // differently, so a plane range (gdm_apply_planes, the overlapped exchange)
-  // must pick the same kernel per plane as the whole launch to give the same
-  // bits (tests/test_host_mpi.py)
-  const bool split = a.z_toep && i1 > i0;
+  // v8: one launch for all output planes, z-wall planes included (each input
+  // plane takes its own z column: wall columns from the LDS table, interior
+  // ones from the compile-time bands, with the same bits in every plane range)
   const int ty = ty8, wgs = wgs8;
   const int64_t tiles = (int64_t)((a.Nx + 63) / 64) * ((a.out_y1 - a.out_y0 + ty - 1) / ty);
   // one round of workgroups on 256 CUs (two rounds measured 0.93 vs 0.85 ms
   // at C3, 0.27 vs 0.22 ms at C4: profiles/r3g/variants.txt)
-  auto zchunk_for = [&](int len) {
-    const int64_t chunks = std::max<int64_t>(1, (256 * wgs + tiles - 1) / tiles);
-    return (int)std::max<int64_t>(std::min(len, 8), (len + chunks - 1) / chunks);
-  };
-  if (!split) {
-    a.cz0[0] = zb; a.cz1[0] = ze; a.cz0[1] = a.cz1[1] = 0;
-    a.zchunk = zchunk_for(ze - zb);
-    a.nchunk0 = (a.cz1[0] - a.cz0[0] + a.zchunk - 1) / a.zchunk;
-    return gdmk_launch_stencil8(p, bk, false, a, op->stream);
-  }
-  gdmk::StencilArgs b = a;
-  b.cz0[0] = i0; b.cz1[0] = i1; b.cz0[1] = b.cz1[1] = 0;
-  b.zchunk = zchunk_for(i1 - i0);
-  b.nchunk0 = (i1 - i0 + b.zchunk - 1) / b.zchunk;
-  hipError_t e = gdmk_launch_stencil8(p, bk, true, b, op->stream);
-  if (e != hipSuccess) return e;
-  // wall ranges [out_z0, i0) and [i1, out_z1)
-  a.cz0[0] = zb; a.cz1[0] = i0;
-  a.cz0[1] = i1; a.cz1[1] = ze;
-  a.zchunk = std::max(1, std::max(i0 - zb, ze - i1));
-  a.nchunk0 = i0 > zb ? 1 : 0;
-  if (i0 <= zb && i1 >= ze) return hipSuccess;
-  return gdmk_launch_stencil8(p, bk, false, a, wall_stream ? wall_stream : op->stream);
+  const int64_t chunks = std::max<int64_t>(1, (256 * wgs + tiles - 1) / tiles);
+  const int len = ze - zb;
+  a.cz0[0] = zb; a.cz1[0] = ze; a.cz0[1] = a.cz1[1] = 0;
+  a.zchunk = (int)std::max<int64_t>(std::min(len, 8), (len + chunks - 1) / chunks);
+  a.nchunk0 = (len + a.zchunk - 1) / a.zchunk;
+  return gdmk_launch_stencil8(op->p, bk, a, op->stream);
 }
 
 // phase 0: both steps on op->stream; 1: step 1 (bc values -> per-face T) on
-// stream `st`; 2: step 2 (T -> dst) on op->stream; 3: both steps into the
-// per-face buffers G on stream `st`; 4: dst += G on op->stream
+// stream `st`; 2: step 2 (T -> dst) on op->stream; 3: every face's step 1 on
+// stream `st`; 4: every face's step 2 + ordered adds into dst on op->stream
 // stage (non-NULL): the boundary values are evaluated from its function
 // (gdm_apply_bc_fn) instead of read from bc_values
 void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
                           hipStream_t st = nullptr) {
   if (op->kind != GDM_OP_ADVECTION) return;
+  if (phase == 0) {
+    // both steps on op->stream: step 1 of every face, then step 2 + adds
+    launch_boundary_data(op, bc_values, dst_owned, 3, op->stream);
+    launch_boundary_data(op, bc_values, dst_owned, 4);
+    return;
+  }
   constexpr int kMax = gdmk::BcStage::kMaxFaces;
   if (op->faces.size() > (size_t)kMax) throw std::runtime_error("more than 6 boundary faces");
   gdmk::FaceArgs fas[kMax] = {};
   int nf = 0;
-  bool all_g = true;
   for (size_t fi = 0; fi < op->faces.size(); ++fi) {
     const Face &F = op->faces[fi];
     if (F.scale == 0.0) continue;
@@ -827,27 +801,25 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     fa.ncell0_total = F.t0.ncell_total;
     fa.cell0_begin = F.t0.cell_begin;
     fa.T = F.T ? F.T : op->face_tmp;
-    fa.G = F.G;
     fa.dst = dst_owned;
     fa.base = F.base;
     fa.stride0 = F.t0.stride;
     fa.stride1 = F.t1.stride;
     fa.scale = F.scale;
     fa.phase = phase;
-    all_g = all_g && F.G && F.T;
     ++nf;
   }
-  // Phase 3 (side stream): every face's step 1 and its step 2 into its own
-  // buffer G while the stencil runs, all faces in one launch per step (each
-  // face has its own T and G); phase 4 adds the buffers into dst face by face
-  // in face order (the same roundings as phase 0's dst += scale s).  Phases
-  // 0 / 4 run one face after the other: two faces share the box-edge nodes,
-  // and a concurrent add (fp64 atomics on the edges) made the edge sums
-  // order-dependent, which the bit-exact rank / communicator comparisons of
-  // tests/test_host_mpi.py catch.
+  // Phase 3 (side stream): every face's step 1 into its own T while the
+  // stencil runs (one launch); phase 4, after the join: every face's step 2
+  // fused with the adds into dst, each node's terms added in face order by
+  // one thread (the roundings of phase 0's face-by-face dst += scale s).  Two
+  // faces share the box-edge nodes: a concurrent add (fp64 atomics on the
+  // edges) made the edge sums order-dependent, which the bit-exact rank /
+  // communicator comparisons of tests/test_host_mpi.py catch.
   const hipStream_t fst = (phase == 1 || phase == 3) && st ? st : op->stream;
-  if (phase == 4 && all_g && op->dim == 3) {
-    // all faces' adds in one launch, the same ordered sums per node
+  bool all_t = true;
+  for (int i = 0; i < nf; ++i) all_t = all_t && fas[i].T != op->face_tmp;
+  if (phase == 4 && all_t && op->dim == 3) {
     gdmk::FaceAddFace ff[kMax] = {};
     int m = 0;
     bool ok = true;
@@ -855,7 +827,6 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
       const Face &F = op->faces[fi];
       if (F.scale == 0.0) continue;
       gdmk::FaceAddFace &a = ff[m++];
-      a.G = F.G;
       a.base = F.base;
       a.stride0 = F.t0.stride;
       a.stride1 = F.t1.stride;
@@ -871,18 +842,21 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     }
     if (ok) {
       const int64_t own_off = (int64_t)op->layout.owned_plane_begin * op->layout.plane_size;
-      const hipError_t e = gdmk_launch_face_adds(ff, m, op->N[0], op->N[1], own_off, dst_owned, op->stream);
+      const hipError_t e =
+          gdmk_launch_faces_step2_add(fas, ff, m, op->N[0], op->N[1], own_off, dst_owned, op->stream);
       if (e == hipSuccess) return;
-      if (e != hipErrorNotSupported) hip_check(e, "face adds");
+      if (e != hipErrorNotSupported) hip_check(e, "face step 2 + adds");
     }
   }
-  if (phase == 3 && all_g) {
-    const hipError_t e = gdmk_launch_faces_g(fas, nf, fst);
+  if (phase == 3 && all_t) {
+    const hipError_t e = gdmk_launch_faces_step1(fas, nf, fst);
     if (e == hipSuccess) return;
-    if (e != hipErrorNotSupported) hip_check(e, "faces launch");
+    if (e != hipErrorNotSupported) hip_check(e, "faces step 1");
   }
+  // face by face: phase 3 = step 1 into T, phase 4 = step 2 from T into dst
   for (int i = 0; i < nf; ++i) {
-    if (phase == 3 && !fas[i].G) fas[i].phase = 1;  // (no buffer: cannot happen for inflow faces)
+    if (phase == 3) fas[i].phase = 1;
+    if (phase == 4) fas[i].phase = 2;
     hip_check(gdmk_launch_face(fas[i], fst), "face launch");
   }
 }
@@ -1467,7 +1441,7 @@ int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const doub
     // interior launch; join before face step 2 adds into dst
     hip_check(hipEventRecord(op->ev_fork, op->stream), "hipEventRecord");
     hip_check(hipStreamWaitEvent(op->side_stream, op->ev_fork, 0), "hipStreamWaitEvent");
-    hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, -1, -1, op->side_stream),
+    hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned),
               "stencil launch");
     if (bc_values) launch_boundary_data(op, bc_values, dst_owned, 3, op->side_stream);
     hip_check(hipEventRecord(op->ev_join, op->side_stream), "hipEventRecord");
@@ -1536,6 +1510,20 @@ int gdm_mass_solve_rk(gdm_op *op, double *rhs_owned, double beta, const double *
   if (op->mesh.n_ranks != 1) return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_rk: single rank");
   if (op->mesh.periodic) return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_rk: periodic constraints");
   if (!rhs_owned || !acc_in || !acc_out || (Y && !y)) return fail(GDM_ERR_ARG, "NULL vector");
+  {
+    // the fused x pass reads rhs one chunk ahead of the stores to acc_out / Y,
+    // and the separate update reads every input element before writing it:
+    // both give the same result only under these aliasing rules
+    const int64_t n = op->layout.n_owned;
+    auto overlap = [n](const double *a, const double *b) { return a && b && a < b + n && b < a + n; };
+    auto partial = [&](const double *a, const double *b) { return overlap(a, b) && a != b; };
+    if (overlap(rhs_owned, acc_in) || overlap(rhs_owned, acc_out) || overlap(rhs_owned, y) || overlap(rhs_owned, Y))
+      return fail(GDM_ERR_ARG, "gdm_mass_solve_rk: rhs_owned overlaps acc_in / acc_out / y / Y");
+    if (overlap(acc_out, Y) || partial(acc_out, acc_in) || partial(acc_out, y) || partial(Y, acc_in) ||
+        partial(Y, y))
+      return fail(GDM_ERR_ARG, "gdm_mass_solve_rk: acc_out / Y must be distinct, or equal (not partially "
+                               "overlapping) to an input");
+  }
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   const gdmk::RkOut rk{acc_in, acc_out, y, Y, beta, alpha};
@@ -1642,12 +1630,15 @@ int gdm_mass_solve_interface_round(gdm_op *op, double *x_local, int round) {
   if (op->layout.n_owned > 0 && !x_local) return fail(GDM_ERR_ARG, "NULL vector");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
-  ++op->spike.next_round;
   const SpikeTables &S = op->spike;
-  hip_check(gdmk_launch_spike(op->p, x_local, op->layout.plane_size,
-                              (int64_t)op->layout.ghost_planes_below * op->layout.plane_size, S.n_planes, S.has_lo,
-                              S.has_hi, S.VW, S.S, S.k_begin, S.k_end, 1, round, S.G0, op->stream),
-            "spike round");
+  // the round counts as done only once its launch succeeded; a failed launch
+  // voids the whole solve (a later interface call then refuses it)
+  const hipError_t e = gdmk_launch_spike(op->p, x_local, op->layout.plane_size,
+                                         (int64_t)op->layout.ghost_planes_below * op->layout.plane_size, S.n_planes,
+                                         S.has_lo, S.has_hi, S.VW, S.S, S.k_begin, S.k_end, 1, round, S.G0, op->stream);
+  if (e != hipSuccess) op->spike.next_round = -1;
+  hip_check(e, "spike round");
+  ++op->spike.next_round;
   return GDM_OK;
   GDM_GUARD_END
 }
@@ -1900,7 +1891,7 @@ int gdm_apply_bc_fn(gdm_op *op, const double *src_local, double *dst_owned, int 
   if (op->concurrent && !op->mesh.periodic) {
     hip_check(hipEventRecord(op->ev_fork, op->stream), "hipEventRecord");
     hip_check(hipStreamWaitEvent(op->side_stream, op->ev_fork, 0), "hipStreamWaitEvent");
-    hip_check(launch_stencil(op, false, src_local, dst_owned, -1, -1, op->side_stream), "stencil launch");
+    hip_check(launch_stencil(op, false, src_local, dst_owned), "stencil launch");
     if (bc) launch_boundary_data(op, bc, dst_owned, 3, op->side_stream);
     hip_check(hipEventRecord(op->ev_join, op->side_stream), "hipEventRecord");
     hip_check(hipStreamWaitEvent(op->stream, op->ev_join, 0), "hipStreamWaitEvent");

@@ -71,13 +71,11 @@ struct FaceArgs {
   const double *phi0;
   const int *crange0;
   int p, ncell0_total, cell0_begin;
-  double *T;  // scratch Q1 x (i0_end - i0_begin)
-  double *G;  // phases 3 / 4: the step-2 result [i1][i0] of the face
+  double *T;  // step-1 result Q1 x (i0_end - i0_begin)
   double *dst;
   int64_t base, stride0, stride1;  // dst offset of node (i0_begin, i1_begin)
   double scale;
-  int phase;  // 0: both steps, 1: step 1 only (writes T), 2: step 2 only (T -> dst),
-              // 3: both steps into G (G = scale s), 4: dst += G
+  int phase;  // 0: both steps, 1: step 1 only (writes T), 2: step 2 only (T -> dst)
 };
 
 // The RK stage update fused into the mass inverse's x pass (gdmk_launch_mass3_rk):
@@ -92,11 +90,10 @@ struct RkOut {
   double beta, alpha;
 };
 
-// phase-4 geometry of one inflow face (gdmk_launch_face_adds): normal axis d
-// at global node coordinate `plane`, tangential axes a0 / a1 (-1 = trivial)
-// with owned node ranges [b0, e0) / [b1, e1); G is [i1 - b1][i0 - b0]
+// node geometry of one inflow face (gdmk_launch_faces_step2_add): normal axis
+// d at global node coordinate `plane`, tangential axes a0 / a1 (-1 = trivial)
+// with owned node ranges [b0, e0) / [b1, e1)
 struct FaceAddFace {
-  const double *G;
   int64_t base, stride0, stride1;  // owned index of node (b0, b1), index strides along a0 / a1
   int d, plane, a0, b0, e0, a1, b1, e1;
 };
@@ -121,8 +118,8 @@ inline hipError_t gdmk_set_lds_attr(const void *kernel, size_t lds, std::atomic<
 
 extern "C" {
 hipError_t gdmk_launch_stencil(int p, int bk, const gdmk::StencilArgs &a, hipStream_t st);
-// zint: every z column of the launch's planes is interior (compile-time z bands)
-hipError_t gdmk_launch_stencil8(int p, int bk, bool zint, const gdmk::StencilArgs &a, hipStream_t st);
+// v8: output planes [cz0[r], cz1[r]) in chunks of zchunk, z-wall planes included
+hipError_t gdmk_launch_stencil8(int p, int bk, const gdmk::StencilArgs &a, hipStream_t st);
 int gdmk_stencil_tile_rows(int p);
 void gdmk_stencil8_geom(int p, int *tile_rows, int *wgs_per_cu);
 hipError_t gdmk_launch_chol_lines(int p, double *v, int len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,
@@ -149,15 +146,12 @@ hipError_t gdmk_launch_mass3_rk(int p, const double *src, int len, int64_t n_lin
                                 const double *urow, const double *invd, const double *cst, int row_lo, int row_hi,
                                 const gdmk::RkOut &rk, hipStream_t st);
 hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st);
-// phase 3 of n inflow faces (step 1 + step 2 into each face's own G) in two
-// launches; hipErrorNotSupported unless every face uses the cell form of step 1
-// with its own T and G (the caller then launches face by face)
-hipError_t gdmk_launch_faces_g(const gdmk::FaceArgs *fa, int n, hipStream_t st);
-// phase 4 of n inflow faces in one launch: every face node gets dst += G of
-// each face containing it, in face order (the node's first face's thread does
-// all of its adds: the same sums as n ordered launches)
-hipError_t gdmk_launch_face_adds(const gdmk::FaceAddFace *f, int n, int64_t N0, int64_t N1, int64_t own_off,
-                                 double *dst, hipStream_t st);
+// step 1 alone of n inflow faces in one launch (cell form, each face its own T)
+hipError_t gdmk_launch_faces_step1(const gdmk::FaceArgs *fa, int n, hipStream_t st);
+// step 2 of n inflow faces from their T, fused with the ordered adds into dst
+// (the sums of face-by-face step-2 launches); fg: the faces' node geometry
+hipError_t gdmk_launch_faces_step2_add(const gdmk::FaceArgs *fa, const gdmk::FaceAddFace *fg, int n, int64_t N0,
+                                       int64_t N1, int64_t own_off, double *dst, hipStream_t st);
 hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st);
 hipError_t gdmk_launch_dot(int64_t n, const double *x, const double *y, double *partial, int n_partial, double *out,
                            hipStream_t st);

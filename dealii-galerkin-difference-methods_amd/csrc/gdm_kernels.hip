@@ -704,6 +704,19 @@ __device__ __forceinline__ constexpr double zband(int k) {
 // the host tables (cy8, zd8, m_zd8: a scale times the band) inherit that
 // exactly, so only p + 1 SGPR pairs stay live (the negation is an operand
 // modifier of the FMA)
+template <int P>
+constexpr bool interior_bands_symmetric() {
+  using IR = InteriorRows<P>;
+  for (int k = 0; k <= 2 * P; ++k)
+    if (IR::m[k] != IR::m[2 * P - k] || IR::l[k] != IR::l[2 * P - k] || IR::c[k] != -IR::c[2 * P - k]) return false;
+  return IR::c[P] == 0.0;
+}
+// hcoef's reconstruction is exact only for exactly (anti)symmetric generated
+// bands (gdm_coeffs.h); a one-ulp asymmetry would change the stencil silently
+static_assert(interior_bands_symmetric<1>() && interior_bands_symmetric<3>() && interior_bands_symmetric<5>() &&
+                  interior_bands_symmetric<7>() && interior_bands_symmetric<9>(),
+              "interior bands must be exactly symmetric (m, l) / antisymmetric (c, c[p] = 0)");
+
 template <int P, int BK>
 __device__ __forceinline__ double hcoef(const double *c, int k) {
   if (k <= P) return c[k];
@@ -1141,7 +1154,7 @@ __device__ __forceinline__ void cblock8(const StencilArgs &a, const Tile7 &t, in
   }
 }
 
-template <int P, int R, int NC, int NP, int BK, int PF, bool ZI, bool YW>
+template <int P, int R, int NC, int NP, int BK, int PF, bool YW>
 __device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7 &t, int ybase, bool full,
                                                bool ywave) {
   using G = Geom8<P, R, NC, NP, BK>;
@@ -1152,17 +1165,25 @@ __device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
   GDM_LDS_BARRIER();  // tables in LDS, counters zeroed
-  // ZI: the host launched this kernel only on output planes whose z columns
-  // are all interior -> compile-time z bands, no table reads; otherwise every
-  // plane reads its column (wall columns or the interior one) from LDS
-  // (one launch for all planes, choosing the compile-time or the table z
-  // column per block of W planes, measured 1.25 vs 0.86 ms at C3: the
-  // consumer loop carries both paths; profiles/r3j/ab_zmix.txt)
-  for (int zb = t.zs; zb < t.zend; zb += W)
-    cblock8<0, P, R, NC, NP, BK, PF, !ZI, YW>(a, t, ybase, full, ywave, acc, zb);
+  // Input plane zz scatters with its z column: a wall column for zz < W or
+  // zz >= Nz - W (LDS table), else the interior one.  Blocks of W planes that
+  // hold a wall column run the table path for all their planes, the others
+  // the compile-time bands; the table's interior row holds exactly the
+  // compile-time coefficients, so a plane gives the same bits in either path,
+  // whatever the launched plane range (gdm_apply_planes, the overlapped
+  // exchange).  The z-wall planes are part of the chunks of this launch: no
+  // second launch with 2p-plane halos of its own.  Three loops, not a branch
+  // per block (a loop carrying both paths measured 1.25 vs 0.86 ms at C3 in
+  // round 3, profiles/r3j/ab_zmix.txt).
+  int zb = t.zs;
+  for (; zb < t.zend && zb < W; zb += W) cblock8<0, P, R, NC, NP, BK, PF, true, YW>(a, t, ybase, full, ywave, acc, zb);
+  const int zhi = a.Nz - 2 * W + 1;  // zb < zhi: no wall column in [zb, zb + W)
+  for (; zb < t.zend && zb < zhi; zb += W)
+    cblock8<0, P, R, NC, NP, BK, PF, false, YW>(a, t, ybase, full, ywave, acc, zb);
+  for (; zb < t.zend; zb += W) cblock8<0, P, R, NC, NP, BK, PF, true, YW>(a, t, ybase, full, ywave, acc, zb);
 }
 
-template <int P, int R, int NC, int NP, int BK, int PF, bool ZI>
+template <int P, int R, int NC, int NP, int BK, int PF>
 __device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) {
   using G = Geom8<P, R, NC, NP, BK>;
   const int ybase = t.y0 + t.cw * R;
@@ -1173,13 +1194,13 @@ __device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) 
   if (t.yedge) {
     const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
     const bool ywave = ybase < ye && ybase + R > yb;
-    consumer8_loop<P, R, NC, NP, BK, PF, ZI, true>(a, t, ybase, full, ywave);
+    consumer8_loop<P, R, NC, NP, BK, PF, true>(a, t, ybase, full, ywave);
   } else {
-    consumer8_loop<P, R, NC, NP, BK, PF, ZI, false>(a, t, ybase, full, false);
+    consumer8_loop<P, R, NC, NP, BK, PF, false>(a, t, ybase, full, false);
   }
 }
 
-template <int P, int R, int NC, int NP, int BK, int CH, int PF, bool ZI>
+template <int P, int R, int NC, int NP, int BK, int CH, int PF>
 __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, NP, BK>::WGS) / 4)
     stencil8_kernel(StencilArgs a) {
   using G = Geom8<P, R, NC, NP, BK>;
@@ -1233,8 +1254,7 @@ __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, N
     t.ncw = t.nl + nr;
   }
   if (threadIdx.x < G::NSYNC) t.sync[threadIdx.x] = 0u;
-  if (!ZI)
-    for (int e = threadIdx.x; e < G::ZTSZ; e += G::NT) t.zt[e] = a.zt[e];
+  for (int e = threadIdx.x; e < G::ZTSZ; e += G::NT) t.zt[e] = a.zt[e];
   if (t.ncw > 0)
     for (int e = threadIdx.x; e < G::CORRSZ; e += G::NT) t.corr[e] = a.corrX[e];
   // y-wall tiles: (wall - Toeplitz) column corrections of the tile rows
@@ -1250,7 +1270,7 @@ __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, N
   if (t.wv < NP)
     producer8<P, R, NC, NP, BK, CH>(a, t);
   else
-    consumer8<P, R, NC, NP, BK, PF, ZI>(a, t);
+    consumer8<P, R, NC, NP, BK, PF>(a, t);
 }
 
 // ---------------------------------------------------------------------------
@@ -1417,7 +1437,7 @@ __global__ void __launch_bounds__(512) face_cell_step1_kernel(const Src U, int Q
 
 // every inflow face's step 1 (cell form) in one launch, face = blockIdx.y:
 // the faces are independent (own T), so their rows share the GPU instead of
-// running one face after the other (gdmk_launch_faces_g)
+// running one face after the other (gdmk_launch_faces_step1)
 template <class Src>
 struct Step1Face {
   Src U;
@@ -1440,13 +1460,9 @@ __global__ void __launch_bounds__(512) face_cell_step1_multi_kernel(const Step1S
                           F.T, blockIdx.x);
 }
 
-// dst node (t, i1) += scale sum_m w1[i1][m] T[q + m][t].  The product is
-// rounded before the add (no FMA contraction into it), so the result equals
-// G = scale s then dst + G (ASSIGN: G written node-major, added by
-// face_add_kernel after the stencil): the same bits on both paths.
 // scale sum_m w1[i1][m] T[q + m][t], the product rounded on its own: the
-// compiler may not fuse it into a later add (one FMA would round differently
-// from G + dst)
+// compiler may not fuse it into the later add (one FMA would round
+// differently from the face-by-face path's dst + G)
 __device__ __forceinline__ double face_step2_value(const double *__restrict__ T, int n0, int t, int i1,
                                                    const int *__restrict__ qs1, const int *__restrict__ qc1,
                                                    const double *__restrict__ w1, int wmax1, double scale) {
@@ -1463,7 +1479,7 @@ __device__ __forceinline__ double face_step2_value(const double *__restrict__ T,
   return v;
 }
 
-template <bool ASSIGN>
+// dst node (t, i1) += scale sum_m w1[i1][m] T[q + m][t]: one face (face by face, in face order)
 __global__ void __launch_bounds__(256) face_step2_kernel(const double *__restrict__ T, int n0, int i1_begin,
                                                           int i1_end, const int *__restrict__ qs1,
                                                           const int *__restrict__ qc1,
@@ -1474,78 +1490,55 @@ __global__ void __launch_bounds__(256) face_step2_kernel(const double *__restric
   const int i1 = i1_begin + (int)blockIdx.y;
   if (t >= n0 || i1 >= i1_end) return;
   const double v = face_step2_value(T, n0, t, i1, qs1, qc1, w1, wmax1, scale);
-  if constexpr (ASSIGN) {
-    dst[(int64_t)(i1 - i1_begin) * n0 + t] = v;
-  } else {
-    double *d = dst + base + (int64_t)t * stride0 + (int64_t)(i1 - i1_begin) * stride1;
-    *d = *d + v;
-  }
+  double *d = dst + base + (int64_t)t * stride0 + (int64_t)(i1 - i1_begin) * stride1;
+  *d = *d + v;
 }
 
-// every inflow face's step 2 into its G in one launch, face = blockIdx.z
+// step-2 data of one face for face_step2_add_kernel
 struct Step2Face {
   const double *T;
   int n0, i1_begin, i1_end;
   const int *qs1, *qc1;
   const double *w1;
   int wmax1;
-  double *G;
   double scale;
-};
-struct Step2Set {
-  Step2Face f[BcStage::kMaxFaces];
-};
-__global__ void __launch_bounds__(256) face_step2_multi_kernel(const Step2Set set) {
-  const Step2Face &F = set.f[blockIdx.z];
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int i1 = F.i1_begin + (int)blockIdx.y;
-  if (t >= F.n0 || i1 >= F.i1_end) return;
-  F.G[(int64_t)(i1 - F.i1_begin) * F.n0 + t] = face_step2_value(F.T, F.n0, t, i1, F.qs1, F.qc1, F.w1, F.wmax1, F.scale);
-}
-
-struct FaceAddSet {
-  FaceAddFace f[BcStage::kMaxFaces];
-  int n;
-  int64_t N0, N1, own_off;
 };
 __device__ __forceinline__ bool face_add_member(const FaceAddFace &g, const int c[3]) {
   return c[g.d] == g.plane && (g.a0 < 0 || (c[g.a0] >= g.b0 && c[g.a0] < g.e0)) &&
          (g.a1 < 0 || (c[g.a1] >= g.b1 && c[g.a1] < g.e1));
 }
-// one thread per node of face blockIdx.z; a node shared with an earlier face
-// is left to that face's thread, which adds every containing face's G in face
-// order: dst + G_f + G_g ..., the sums of the ordered per-face launches
-__global__ void __launch_bounds__(256) face_add_multi_kernel(const FaceAddSet set, double *__restrict__ dst) {
+// step 2 of every inflow face fused with the ordered adds (one launch, face =
+// blockIdx.z): a node is handled by the thread of the first face containing
+// it, which adds its own face's G = scale sum_m w1 T and then every later
+// containing face's G, in face order -- the sums (and roundings) of the
+// per-face step-2 launches, without the G buffers and the separate add launch
+struct Step2AddSet {
+  Step2Face f[BcStage::kMaxFaces];
+  FaceAddFace g[BcStage::kMaxFaces];
+  int n;
+  int64_t N0, N1, own_off;
+};
+__global__ void __launch_bounds__(256) face_step2_add_kernel(const Step2AddSet set, double *__restrict__ dst) {
   const int f = blockIdx.z;
-  const FaceAddFace &F = set.f[f];
-  const int n0 = F.e0 - F.b0;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x, i1 = blockIdx.y;
-  if (t >= n0 || i1 >= F.e1 - F.b1) return;
-  const int64_t o = F.base + (int64_t)t * F.stride0 + (int64_t)i1 * F.stride1;
+  const Step2Face &F = set.f[f];
+  const FaceAddFace &A = set.g[f];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y;
+  if (t >= F.n0 || F.i1_begin + r >= F.i1_end) return;
+  const int64_t o = A.base + (int64_t)t * A.stride0 + (int64_t)r * A.stride1;
   const int64_t gi = o + set.own_off;
   const int c[3] = {(int)(gi % set.N0), (int)((gi / set.N0) % set.N1), (int)(gi / (set.N0 * set.N1))};
   for (int g = 0; g < f; ++g)
-    if (face_add_member(set.f[g], c)) return;
+    if (face_add_member(set.g[g], c)) return;
   double v = dst[o];
-  v = v + F.G[(int64_t)i1 * n0 + t];
+  v = v + face_step2_value(F.T, F.n0, t, F.i1_begin + r, F.qs1, F.qc1, F.w1, F.wmax1, F.scale);
   for (int g = f + 1; g < set.n; ++g) {
-    const FaceAddFace &H = set.f[g];
+    const FaceAddFace &H = set.g[g];
     if (!face_add_member(H, c)) continue;
+    const Step2Face &S = set.f[g];
     const int u0 = H.a0 < 0 ? 0 : c[H.a0] - H.b0, u1 = H.a1 < 0 ? 0 : c[H.a1] - H.b1;
-    v = v + H.G[(int64_t)u1 * (H.e0 - H.b0) + u0];
+    v = v + face_step2_value(S.T, S.n0, u0, S.i1_begin + u1, S.qs1, S.qc1, S.w1, S.wmax1, S.scale);
   }
   dst[o] = v;
-}
-
-// dst node (t, i1) += G[i1][t]: one launch per face, in face order
-__global__ void __launch_bounds__(256) face_add_kernel(const double *__restrict__ G, int n0, int n1,
-                                                        double *__restrict__ dst, int64_t base, int64_t stride0,
-                                                        int64_t stride1) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)n0 * n1) return;
-  const int i1 = (int)(e / n0), t = (int)(e - (int64_t)i1 * n0);
-  double *d = dst + base + (int64_t)t * stride0 + (int64_t)i1 * stride1;
-  *d = *d + G[e];
 }
 
 // ---------------------------------------------------------------------------
@@ -1634,7 +1627,7 @@ static hipError_t launch7_p(int bk, const StencilArgs &a, hipStream_t st) {
   }
 }
 
-template <int P, int R, int NC, int NP, int BK, int CH, int PF, bool ZI>
+template <int P, int R, int NC, int NP, int BK, int CH, int PF>
 static hipError_t launch8_t(const StencilArgs &a, hipStream_t st) {
   using G = Geom8<P, R, NC, NP, BK>;
   static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget");
@@ -1642,7 +1635,7 @@ static hipError_t launch8_t(const StencilArgs &a, hipStream_t st) {
   {
     // the LDS attribute is per device; one bit per device, set from any thread
     static std::atomic<uint64_t> attr_mask{0};
-    hipError_t e = gdmk_set_lds_attr((const void *)stencil8_kernel<P, R, NC, NP, BK, CH, PF, ZI>, lds, attr_mask);
+    hipError_t e = gdmk_set_lds_attr((const void *)stencil8_kernel<P, R, NC, NP, BK, CH, PF>, lds, attr_mask);
     if (e != hipSuccess) return e;
   }
   int nz = 0;
@@ -1650,49 +1643,44 @@ static hipError_t launch8_t(const StencilArgs &a, hipStream_t st) {
     if (a.cz1[r] > a.cz0[r]) nz += (a.cz1[r] - a.cz0[r] + a.zchunk - 1) / a.zchunk;
   dim3 grid((a.Nx + G::TX - 1) / G::TX, (a.out_y1 - a.out_y0 + G::TY - 1) / G::TY, nz);
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return hipSuccess;
-  hipLaunchKernelGGL((stencil8_kernel<P, R, NC, NP, BK, CH, PF, ZI>), grid, dim3(G::NT), lds, st, a);
+  hipLaunchKernelGGL((stencil8_kernel<P, R, NC, NP, BK, CH, PF>), grid, dim3(G::NT), lds, st, a);
   return hipGetLastError();
 }
 
-template <int P, int R, int NC, int NP, int PF, bool ZI>
-static hipError_t launch8_z(int bk, const StencilArgs &a, hipStream_t st) {
+template <int P, int R, int NC, int NP, int PF>
+static hipError_t launch8_p(int bk, const StencilArgs &a, hipStream_t st) {
   const bool vec = (a.Nx % 2 == 0) && ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0);
   switch (bk) {
 #ifdef GDM_ONLY_ADV16  // fast experiment builds: advection, 16-B DMA only
-    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF, ZI>(a, st) : hipErrorInvalidValue;
+    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF>(a, st) : hipErrorInvalidValue;
 #else
-    case 0: return vec ? launch8_t<P, R, NC, NP, 0, 16, PF, ZI>(a, st) : launch8_t<P, R, NC, NP, 0, 4, PF, ZI>(a, st);
-    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF, ZI>(a, st) : launch8_t<P, R, NC, NP, 1, 4, PF, ZI>(a, st);
-    case 2: return vec ? launch8_t<P, R, NC, NP, 2, 16, PF, ZI>(a, st) : launch8_t<P, R, NC, NP, 2, 4, PF, ZI>(a, st);
+    case 0: return vec ? launch8_t<P, R, NC, NP, 0, 16, PF>(a, st) : launch8_t<P, R, NC, NP, 0, 4, PF>(a, st);
+    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF>(a, st) : launch8_t<P, R, NC, NP, 1, 4, PF>(a, st);
+    case 2: return vec ? launch8_t<P, R, NC, NP, 2, 16, PF>(a, st) : launch8_t<P, R, NC, NP, 2, 4, PF>(a, st);
 #endif
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int P, int R, int NC, int NP, int PF>
-static hipError_t launch8_p(int bk, bool zint, const StencilArgs &a, hipStream_t st) {
-  return zint ? launch8_z<P, R, NC, NP, PF, true>(bk, a, st) : launch8_z<P, R, NC, NP, PF, false>(bk, a, st);
-}
-
 }  // namespace gdmk
 
-extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, bool zint, const gdmk::StencilArgs &a, hipStream_t st) {
+extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, const gdmk::StencilArgs &a, hipStream_t st) {
   using namespace gdmk;
   switch (p) {
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 1
-    case 1: return launch8_p<1, 4, 8, 8, 3>(bk, zint, a, st);
+    case 1: return launch8_p<1, 4, 8, 8, 3>(bk, a, st);
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 3
-    case 3: return launch8_p<3, 4, 8, 8, 3>(bk, zint, a, st);
+    case 3: return launch8_p<3, 4, 8, 8, 3>(bk, a, st);
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 5
-    case 5: return launch8_p<5, GDM_R5, GDM_NC5, GDM_NP5, GDM_PF5>(bk, zint, a, st);
+    case 5: return launch8_p<5, GDM_R5, GDM_NC5, GDM_NP5, GDM_PF5>(bk, a, st);
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 7
-    case 7: return launch8_p<7, GDM_R7, GDM_NC7, GDM_NP7, GDM_PF7>(bk, zint, a, st);
+    case 7: return launch8_p<7, GDM_R7, GDM_NC7, GDM_NP7, GDM_PF7>(bk, a, st);
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 9
-    case 9: return launch8_p<9, 2, 8, 8, 3>(bk, zint, a, st);
+    case 9: return launch8_p<9, 2, 8, 8, 3>(bk, a, st);
 #endif
     
     default: return hipErrorInvalidValue;
@@ -1811,92 +1799,73 @@ extern "C" hipError_t gdmk_launch_face(const gdmk::FaceArgs &f, hipStream_t st) 
   using namespace gdmk;
   const int n0 = f.i0_end - f.i0_begin;
   if (n0 <= 0 || f.Q1 <= 0 || f.i1_end <= f.i1_begin) return hipSuccess;
-  if (f.phase == 4) {
-    const int n1 = f.i1_end - f.i1_begin;
-    const int64_t ne = (int64_t)n0 * n1;
-    hipLaunchKernelGGL(face_add_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, f.G, n0, n1, f.dst,
-                       f.base, f.stride0, f.stride1);
-    return hipGetLastError();
-  }
+  if (f.phase < 0 || f.phase > 2) return hipErrorInvalidValue;
   auto step2 = [&](dim3 g2) {
-    if (f.phase == 3)
-      hipLaunchKernelGGL(face_step2_kernel<true>, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1,
-                         f.w1, f.wmax1, f.G, (int64_t)0, (int64_t)1, (int64_t)n0, f.scale);
-    else
-      hipLaunchKernelGGL(face_step2_kernel<false>, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1,
-                         f.w1, f.wmax1, f.dst, f.base, f.stride0, f.stride1, f.scale);
+    hipLaunchKernelGGL(face_step2_kernel, g2, dim3(256), 0, st, f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1,
+                       f.wmax1, f.dst, f.base, f.stride0, f.stride1, f.scale);
   };
   return face_launch(f, BcArr{f.U, f.Q0}, st, step2);
 }
 
-
-template <class Src, class Get>
-static hipError_t faces_g_launch(const gdmk::FaceArgs *fa, int n, Get &&src, hipStream_t st) {
+// step 1 (cell form) of n inflow faces in one launch (each face its own T)
+extern "C" hipError_t gdmk_launch_faces_step1(const gdmk::FaceArgs *fa, int n, hipStream_t st) {
   using namespace gdmk;
-  Step1Set<Src> s1{};
-  Step2Set s2{};
+  if (n <= 0) return hipSuccess;
+  if (n > BcStage::kMaxFaces) return hipErrorNotSupported;
+  Step1Set<BcArr> s1{};
   s1.rpb = 4;
   size_t lds = 0;
-  int g1 = 0, g2x = 0, g2y = 0;
+  int g1 = 0;
   for (int i = 0; i < n; ++i) {
     const FaceArgs &f = fa[i];
-    const int n0 = f.i0_end - f.i0_begin;
-    s1.f[i] = Step1Face<Src>{src(f), f.Q0, f.Q1, f.i0_begin, n0, f.crange0, f.phi0, f.ncell0_total, f.cell0_begin,
-                             f.T};
-    s2.f[i] = Step2Face{f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1, f.G, f.scale};
-    lds = std::max(lds, sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)f.Q0));
+    const size_t cell_lds = sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)f.Q0);
+    if (!f.phi0 || cell_lds > 48 * 1024 || !f.T || f.p != fa[0].p || f.Q1 <= 0 || f.i0_end <= f.i0_begin)
+      return hipErrorNotSupported;
+    for (int j = 0; j < i; ++j)
+      if (fa[j].T == f.T) return hipErrorNotSupported;  // faces must not share T
+    s1.f[i] = Step1Face<BcArr>{BcArr{f.U, f.Q0}, f.Q0, f.Q1, f.i0_begin, f.i0_end - f.i0_begin, f.crange0, f.phi0,
+                               f.ncell0_total, f.cell0_begin, f.T};
+    lds = std::max(lds, cell_lds);
     g1 = std::max(g1, (f.Q1 + s1.rpb - 1) / s1.rpb);
-    g2x = std::max(g2x, (n0 + 255) / 256);
-    g2y = std::max(g2y, f.i1_end - f.i1_begin);
   }
   switch (fa[0].p) {
-#define GDM_FACES_G(PP)                                                                                   \
-  case PP:                                                                                              \
-    hipLaunchKernelGGL((face_cell_step1_multi_kernel<PP, Src>), dim3(g1, n), dim3(512), lds, st, s1); \
+#define GDM_FACES_S1(PP)                                                                                       \
+  case PP:                                                                                                   \
+    hipLaunchKernelGGL((face_cell_step1_multi_kernel<PP, BcArr>), dim3(g1, n), dim3(512), lds, st, s1); \
     break;
-    GDM_FACES_G(1) GDM_FACES_G(3) GDM_FACES_G(5) GDM_FACES_G(7) GDM_FACES_G(9)
-#undef GDM_FACES_G
+    GDM_FACES_S1(1) GDM_FACES_S1(3) GDM_FACES_S1(5) GDM_FACES_S1(7) GDM_FACES_S1(9)
+#undef GDM_FACES_S1
     default: return hipErrorNotSupported;
   }
-  hipLaunchKernelGGL(face_step2_multi_kernel, dim3(g2x, g2y, n), dim3(256), 0, st, s2);
   return hipGetLastError();
 }
 
-extern "C" hipError_t gdmk_launch_face_adds(const gdmk::FaceAddFace *f, int n, int64_t N0, int64_t N1,
-                                            int64_t own_off, double *dst, hipStream_t st) {
+// step 2 of n inflow faces (their T from gdmk_launch_faces_step1) with the
+// ordered adds into dst, one launch (face_step2_add_kernel)
+extern "C" hipError_t gdmk_launch_faces_step2_add(const gdmk::FaceArgs *fa, const gdmk::FaceAddFace *fg, int n,
+                                                  int64_t N0, int64_t N1, int64_t own_off, double *dst,
+                                                  hipStream_t st) {
   using namespace gdmk;
   if (n <= 0) return hipSuccess;
   if (n > BcStage::kMaxFaces || N0 <= 0 || N1 <= 0) return hipErrorNotSupported;
-  FaceAddSet set{};
+  Step2AddSet set{};
   set.n = n;
   set.N0 = N0;
   set.N1 = N1;
   set.own_off = own_off;
   int gx = 0, gy = 0;
   for (int i = 0; i < n; ++i) {
-    set.f[i] = f[i];
-    gx = std::max(gx, (f[i].e0 - f[i].b0 + 255) / 256);
-    gy = std::max(gy, f[i].e1 - f[i].b1);
+    const FaceArgs &f = fa[i];
+    const int n0 = f.i0_end - f.i0_begin;
+    if (!f.T || fg[i].e0 - fg[i].b0 != n0 || fg[i].e1 - fg[i].b1 != f.i1_end - f.i1_begin) return hipErrorNotSupported;
+    set.f[i] = Step2Face{f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1, f.scale};
+    set.g[i] = fg[i];
+    gx = std::max(gx, (n0 + 255) / 256);
+    gy = std::max(gy, f.i1_end - f.i1_begin);
   }
   if (gx <= 0 || gy <= 0) return hipSuccess;
-  hipLaunchKernelGGL(face_add_multi_kernel, dim3(gx, gy, n), dim3(256), 0, st, set, dst);
+  hipLaunchKernelGGL(face_step2_add_kernel, dim3(gx, gy, n), dim3(256), 0, st, set, dst);
   return hipGetLastError();
-}
-
-extern "C" hipError_t gdmk_launch_faces_g(const gdmk::FaceArgs *fa, int n, hipStream_t st) {
-  using namespace gdmk;
-  if (n <= 0) return hipSuccess;
-  if (n > BcStage::kMaxFaces) return hipErrorNotSupported;
-  for (int i = 0; i < n; ++i) {
-    const FaceArgs &f = fa[i];
-    const size_t cell_lds = sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)f.Q0);
-    if (!f.phi0 || cell_lds > 48 * 1024 || !f.G || !f.T || f.p != fa[0].p || f.Q1 <= 0 ||
-        f.i0_end <= f.i0_begin || f.i1_end <= f.i1_begin)
-      return hipErrorNotSupported;
-    for (int j = 0; j < i; ++j)
-      if (fa[j].T == f.T || fa[j].G == f.G) return hipErrorNotSupported;  // faces must not share buffers
-  }
-  return faces_g_launch<BcArr>(fa, n, [](const FaceArgs &f) { return BcArr{f.U, f.Q0}; }, st);
 }
 
 extern "C" hipError_t gdmk_launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st) {

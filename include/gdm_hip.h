@@ -145,8 +145,14 @@ typedef struct {
 
 /* params (n_params):
  *   GDM_OP_MASS        : none
- *   GDM_OP_ADVECTION   : a_x, a_y, a_z               (constant field)
+ *   GDM_OP_ADVECTION   : a_x, a_y, a_z               (constant field, see below)
  *   GDM_OP_CONVECTIVE  : a_x, a_y, a_z
+ *   The reference evaluates advection->value(x_q, d) at every quadrature point
+ *   (advection/stiffness.h:395-406, 443, 510); the engine's Kronecker form
+ *   holds for a CONSTANT field only, which is what every reference preset uses
+ *   (ConstantFunction, advection-app.cc:131-139).  A spatially varying field
+ *   cannot be expressed through these params: a caller with one must keep the
+ *   reference's cell loop (the engine cannot detect it, it only sees a[]).
  *   GDM_OP_WAVE        : [nitsche_parameter]         (> 0 enables box Nitsche,
  *                        function_domain_dbc; absent / <= 0 = natural BC) */
 int gdm_last_error(char *buf, size_t len);
@@ -193,8 +199,11 @@ int gdm_mass_solve(gdm_op *op, const double *rhs_owned, double *x_owned);
  * beta k and, when Y != NULL, Y = y + alpha k -- one RK stage's solve and
  * update (advection/problem.h:62-94 + the solve of :236-267) with the update
  * fused into the last line-solve pass, so k never reaches HBM.  rhs_owned is
- * overwritten (scratch); acc_in may equal acc_out.  Same bits as
- * gdm_mass_solve(rhs, rhs) + gdm_vec_rk_update.  Single rank, non-periodic. */
+ * overwritten (scratch).  Aliasing (GDM_ERR_ARG otherwise): rhs_owned overlaps
+ * none of acc_in / acc_out / y / Y; acc_out and Y are distinct; a written
+ * vector (acc_out, Y) may equal a read one (acc_in, y) but not partially
+ * overlap it.  Same bits as gdm_mass_solve(rhs, rhs) + gdm_vec_rk_update.
+ * Single rank, non-periodic. */
 int gdm_mass_solve_rk(gdm_op *op, double *rhs_owned, double beta, const double *acc_in, double *acc_out,
                       double alpha, const double *y, double *Y);
 

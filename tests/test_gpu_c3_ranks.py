@@ -1,0 +1,90 @@
+"""BASELINE config C3 at its named split: the 512^3 p = 5 advection grid on
+8 z-slab ranks (system.h:720-757), all eight rank operators built in one
+process and evaluated the way bench.py / apply_overlapped run them at N = 8,
+the ghost exchange done by copying the neighbours' planes from the global
+vector (what HaloExchange moves over RCCL).
+
+* compute_rhs (advection/stiffness.h:343 + :345-605): interior planes while
+  the exchange would be in flight, the p planes next to each slab edge after
+  it, then the inflow data of the rank's device boundary points -- against the
+  single-rank application of the whole grid, rel-L2 <= 1e-12;
+* the distributed exact mass inverse (truncated SPIKE: slab solve + interface
+  correction, problem.h:236-267's solve) against the single-rank Kronecker
+  inverse, rel-L2 <= 1e-13.
+
+Both single-rank references are pinned to the oracle at this size elsewhere
+(tests/test_gpu_fullsize.py).  Peak device memory ~6 GB."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+N_CELLS, P, R = 511, 5, 8
+A = (1.0, 0.15, -0.05)
+
+
+def _rel(a, b):
+    return float(torch.linalg.norm(a - b) / torch.linalg.norm(b))
+
+
+def test_c3_eight_ranks_compute_rhs_and_spike_match_single_rank():
+    import gdm_amd
+    from gdm_amd.distributed import apply_overlapped
+
+    full = gdm_amd.GdmOperator(3, P, N_CELLS, 0.0, 1.0, "advection", params=A)
+    ps = full.layout["plane_size"]
+    gen = torch.Generator("cuda").manual_seed(11)
+    u = torch.rand(full.n_owned, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+
+    def bc_for(op):  # smooth inflow data at the operator's device boundary points
+        x = op.bc_points()
+        return torch.from_numpy(np.sin(3 * x[:, 0] + 1) * np.cos(2 * x[:, 1] - 0.5) + x[:, 2]).cuda()
+
+    ref = full.new_vector(local=False)
+    full.apply(u, ref, bc_for(full))
+    m_ref = full.new_vector(local=False)
+    full.mass_solve(ref, m_ref)
+    torch.cuda.synchronize()
+    del full
+
+    out = torch.empty_like(ref)
+    xs, ops = [], []
+    for r in range(R):
+        op = gdm_amd.GdmOperator(3, P, N_CELLS, 0.0, 1.0, "advection", params=A, rank=r, n_ranks=R)
+        L = op.layout
+        first = L["owned_plane_begin"] - L["ghost_planes_below"]
+        local = u[first * ps:first * ps + L["n_local"]].clone()
+        y = op.new_vector(local=False)
+        apply_overlapped(op, None, local, y, bc_for(op))
+        b = L["owned_plane_begin"] * ps
+        out[b:b + L["n_owned"]] = y
+        # the SPIKE slab solve of this rank's share of the single-rank rhs
+        x = op.new_vector(True)
+        op.mass_solve_slab(ref[b:b + L["n_owned"]].contiguous(), op.owned_view(x))
+        xs.append(x)
+        ops.append(op)
+        del local, y
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 1e-12
+
+    def exchange():
+        for r, op in enumerate(ops):
+            L = op.layout
+            gb, ga, own = L["ghost_planes_below"], L["ghost_planes_above"], L["n_owned"] // ps
+            if r > 0 and gb:
+                Ln = ops[r - 1].layout
+                e = (Ln["ghost_planes_below"] + Ln["n_owned"] // ps) * ps
+                xs[r][:gb * ps] = xs[r - 1][e - gb * ps:e]
+            if r + 1 < R and ga:
+                Ln = ops[r + 1].layout
+                b = Ln["ghost_planes_below"] * ps
+                xs[r][(gb + own) * ps:(gb + own + ga) * ps] = xs[r + 1][b:b + ga * ps]
+
+    rounds = gdm_amd._capi.mass_spike_rounds(3, P, N_CELLS, R)
+    assert rounds == 0  # 64-plane slabs at p = 5: far-spike coupling 6e-21, no refinement round
+    exchange()
+    for op, x in zip(ops, xs):
+        op.mass_solve_interface(x)
+    got = torch.cat([op.owned_view(x) for op, x in zip(ops, xs)])
+    assert _rel(got, m_ref) < 1e-13

@@ -2,9 +2,10 @@
 # Experiment build for an on-box A/B of the stencil:
 #   tools/build_variant.sh NAME [hipcc -D flags...]  -> dealii-galerkin-difference-methods_amd/lib/ab/NAME/libgdm_hip.so
 # gdm_kernels.hip is rebuilt with the flags (ONLY_P=5 by default: that degree's
-# stencil only; ONLY_ADV16=1: advection with 16-B DMA only), every other object
-# comes from the in-tree build (lib/obj).  Select it with GDM_HIP_LIB (tools/gpu_ab.sh,
-# tools/time_apply.py) and delete lib/ab/NAME when the experiment is recorded.
+# stencil only; ONLY_ADV16=1: advection with 16-B DMA only; BUILD_CAPI=1: gdm_capi.cpp
+# too), every other object comes from the in-tree build (lib/obj).  Select it
+# with GDM_HIP_LIB (tools/gpu_ab.sh, tools/time_apply.py) and delete
+# lib/ab/NAME when the experiment is recorded.
 NAME=$1; shift
 C=/root/repo/dealii-galerkin-difference-methods_amd/csrc
 B=/root/repo/dealii-galerkin-difference-methods_amd/lib/obj
@@ -13,7 +14,12 @@ mkdir -p $O
 X=""
 [ "${ONLY_ADV16:-0}" = 1 ] && X="-DGDM_ONLY_ADV16"
 F="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -Wno-unused-function -DGDM_ONLY_P=${ONLY_P:-5} $X $*"
+CAPI=$B/gdm_capi.o
+if [ "${BUILD_CAPI:-0}" = 1 ]; then
+  /opt/rocm/bin/hipcc $F -x hip -c $C/gdm_capi.cpp -o $O/capi.o || exit 1
+  CAPI=$O/capi.o
+fi
 /opt/rocm/bin/hipcc $F -c $C/gdm_kernels.hip -o $O/kernels.o &&
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libgdm_hip.so $B/gdm_capi.o $O/kernels.o $B/gdm_setup.o \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libgdm_hip.so $CAPI $O/kernels.o $B/gdm_setup.o \
   $B/gdm_csr.o $B/gdm_mass.o $B/gdm_rk.o $B/gdm_post.o $B/gdm_cut.o $B/gdm_cut_advection.o $B/gdm_cut_wave.o \
-  $B/gdm_band.o && rm -f $O/kernels.o && echo "built $O"
+  $B/gdm_band.o && rm -f $O/kernels.o $O/capi.o && echo "built $O"
