@@ -112,11 +112,7 @@ struct SpikeTables {
 struct gdm_op {
   int device = 0;
   hipStream_t own_stream = nullptr, stream = nullptr;
-  // fork / join of gdm_apply: the z-wall stencil launch and the inflow face
-  // step 1 run on side_stream, filling the tail of the interior launch
-  hipStream_t side_stream = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  bool concurrent = true;  // fork / join of the z-wall launch and face step 1 on the side stream
+  bool concurrent = true;  // compute_rhs: face step 1 in the stencil's tail (apply_with_faces)
   gdm_mesh_desc mesh{};
   int kind = 0, p = 1, dim = 1;
   int N[3] = {1, 1, 1};        // vertices per reference direction
@@ -162,6 +158,10 @@ struct gdm_op {
   double *cg_r = nullptr, *cg_p = nullptr, *cg_Ap = nullptr, *cg_z = nullptr, *cg_invdiag = nullptr;
   std::vector<Face> faces;
   double *face_tmp = nullptr;
+  // the stencil's tail work (face step 1, gdmk_launch_stencil8): device claim
+  // counter and the next launch's first claim
+  unsigned long long *tail_counter = nullptr;
+  unsigned long long tail_base = 0;
   double *mass_tmp = nullptr;  // ping-pong vector of the segmented mass passes (small meshes)
   int64_t mass_tmp_size = 0;
   int64_t face_tmp_size = 0;
@@ -180,9 +180,6 @@ void free_op(gdm_op *op) {
   if (!op) return;
   for (void *ptr : op->allocations) (void)hipFree(ptr);
   if (op->own_stream) (void)hipStreamDestroy(op->own_stream);
-  if (op->side_stream) (void)hipStreamDestroy(op->side_stream);
-  if (op->ev_fork) (void)hipEventDestroy(op->ev_fork);
-  if (op->ev_join) (void)hipEventDestroy(op->ev_join);
   delete op;
 }
 
@@ -676,7 +673,11 @@ void build_faces(gdm_op *op) {
 
 // Output planes [zb, ze) of the owned range (3D: z planes; the full owned
 // range otherwise).  dst is the owned vector; only those planes are written.
-hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst, int zb = -1, int ze = -1) {
+// tail / n_tail: inflow faces whose step 1 the stencil's workgroups run once
+// their chunk is done (v8 only); *tail_done reports whether it ran
+hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst, int zb = -1, int ze = -1,
+                          const gdmk::FaceArgs *tail = nullptr, int n_tail = 0, bool *tail_done = nullptr) {
+  if (tail_done) *tail_done = false;
   const gdm_layout &L = op->layout;
   gdmk::StencilArgs a{};
   a.src = src;
@@ -754,26 +755,21 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
   a.cz0[0] = zb; a.cz1[0] = ze; a.cz0[1] = a.cz1[1] = 0;
   a.zchunk = (int)std::max<int64_t>(std::min(len, 8), (len + chunks - 1) / chunks);
   a.nchunk0 = (len + a.zchunk - 1) / a.zchunk;
-  return gdmk_launch_stencil8(op->p, bk, a, op->stream);
+  const bool with_tail = n_tail > 0 && tail && op->tail_counter;
+  unsigned long long claims = 0;
+  const hipError_t e = gdmk_launch_stencil8(op->p, bk, a, with_tail ? tail : nullptr, with_tail ? n_tail : 0,
+                                            op->tail_counter, op->tail_base, &claims, op->stream);
+  if (e == hipSuccess) {
+    op->tail_base += claims;
+    if (tail_done) *tail_done = claims > 0;
+  }
+  return e;
 }
 
-// phase 0: both steps on op->stream; 1: step 1 (bc values -> per-face T) on
-// stream `st`; 2: step 2 (T -> dst) on op->stream; 3: every face's step 1 on
-// stream `st`; 4: every face's step 2 + ordered adds into dst on op->stream
-// stage (non-NULL): the boundary values are evaluated from its function
-// (gdm_apply_bc_fn) instead of read from bc_values
-void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
-                          hipStream_t st = nullptr) {
-  if (op->kind != GDM_OP_ADVECTION) return;
-  if (phase == 0) {
-    // both steps on op->stream: step 1 of every face, then step 2 + adds
-    launch_boundary_data(op, bc_values, dst_owned, 3, op->stream);
-    launch_boundary_data(op, bc_values, dst_owned, 4);
-    return;
-  }
+// the inflow faces' launch arguments (faces with |a.n| > 0, in face order)
+int face_args(gdm_op *op, const double *bc_values, double *dst_owned, int phase, gdmk::FaceArgs *fas) {
   constexpr int kMax = gdmk::BcStage::kMaxFaces;
   if (op->faces.size() > (size_t)kMax) throw std::runtime_error("more than 6 boundary faces");
-  gdmk::FaceArgs fas[kMax] = {};
   int nf = 0;
   for (size_t fi = 0; fi < op->faces.size(); ++fi) {
     const Face &F = op->faces[fi];
@@ -809,6 +805,26 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     fa.phase = phase;
     ++nf;
   }
+  return nf;
+}
+
+// phase 0: both steps on op->stream; 1: step 1 (bc values -> per-face T) on
+// stream `st`; 2: step 2 (T -> dst) on op->stream; 3: every face's step 1 on
+// stream `st`; 4: every face's step 2 + ordered adds into dst on op->stream
+// stage (non-NULL): the boundary values are evaluated from its function
+// (gdm_apply_bc_fn) instead of read from bc_values
+void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned, int phase = 0,
+                          hipStream_t st = nullptr) {
+  if (op->kind != GDM_OP_ADVECTION) return;
+  if (phase == 0) {
+    // both steps on op->stream: step 1 of every face, then step 2 + adds
+    launch_boundary_data(op, bc_values, dst_owned, 3, op->stream);
+    launch_boundary_data(op, bc_values, dst_owned, 4);
+    return;
+  }
+  constexpr int kMax = gdmk::BcStage::kMaxFaces;
+  gdmk::FaceArgs fas[kMax] = {};
+  const int nf = face_args(op, bc_values, dst_owned, phase, fas);
   // Phase 3 (side stream): every face's step 1 into its own T while the
   // stencil runs (one launch); phase 4, after the join: every face's step 2
   // fused with the adds into dst, each node's terms added in face order by
@@ -859,6 +875,29 @@ void launch_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned
     if (phase == 4) fas[i].phase = 2;
     hip_check(gdmk_launch_face(fas[i], fst), "face launch");
   }
+}
+
+// compute_rhs = stencil + inflow data.  The inflow faces' step 1 runs in the
+// tail of the stencil launch (its workgroups take the face rows once their
+// chunk is done); where that is not available (v7 meshes) after the stencil;
+// then step 2 with the ordered adds.
+void apply_with_faces(gdm_op *op, bool mass, const double *src_local, double *dst_owned, const double *bc_values) {
+  constexpr int kMax = gdmk::BcStage::kMaxFaces;
+  gdmk::FaceArgs fas[kMax] = {};
+  const int nf = bc_values && op->kind == GDM_OP_ADVECTION ? face_args(op, bc_values, dst_owned, 1, fas) : 0;
+  bool tail_done = false;
+  if (nf > 0) {
+    hip_check(launch_stencil(op, mass, src_local, dst_owned, -1, -1, fas, nf, &tail_done), "stencil launch");
+    if (tail_done) {
+      launch_boundary_data(op, bc_values, dst_owned, 4);
+      return;
+    }
+    // the stencil ran without the tail work: step 1 after it
+    launch_boundary_data(op, bc_values, dst_owned, 3, op->stream);
+    launch_boundary_data(op, bc_values, dst_owned, 4);
+    return;
+  }
+  hip_check(launch_stencil(op, mass, src_local, dst_owned), "stencil launch");
 }
 
 int choose_zchunk(const gdm_op *op) {
@@ -1253,9 +1292,9 @@ int gdm_op_create(const gdm_mesh_desc *mesh, int kind, const double *params, int
   hip_check(hipSetDevice(device), "hipSetDevice");
   hip_check(hipStreamCreateWithFlags(&op->own_stream, hipStreamNonBlocking), "hipStreamCreate");
   op->stream = op->own_stream;
-  hip_check(hipStreamCreateWithFlags(&op->side_stream, hipStreamNonBlocking), "hipStreamCreate");
-  hip_check(hipEventCreateWithFlags(&op->ev_fork, hipEventDisableTiming), "hipEventCreate");
-  hip_check(hipEventCreateWithFlags(&op->ev_join, hipEventDisableTiming), "hipEventCreate");
+  hip_check(hipMalloc(&op->tail_counter, sizeof(unsigned long long)), "hipMalloc");
+  keep(op, op->tail_counter);
+  hip_check(hipMemset(op->tail_counter, 0, sizeof(unsigned long long)), "hipMemset");
   build_layout(op);
   build_tables(op);
   build_faces(op);
@@ -1281,7 +1320,6 @@ int gdm_op_destroy(gdm_op *op) {
   if (!op) return GDM_OK;
   (void)hipSetDevice(op->device);
   if (op->own_stream) (void)hipStreamSynchronize(op->own_stream);
-  if (op->side_stream) (void)hipStreamSynchronize(op->side_stream);
   free_op(op);
   return GDM_OK;
 }
@@ -1437,16 +1475,7 @@ int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const doub
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   if (op->concurrent && !op->mesh.periodic) {
-    // fork: z-wall launch + face step 1 on the side stream fill the tail of the
-    // interior launch; join before face step 2 adds into dst
-    hip_check(hipEventRecord(op->ev_fork, op->stream), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(op->side_stream, op->ev_fork, 0), "hipStreamWaitEvent");
-    hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned),
-              "stencil launch");
-    if (bc_values) launch_boundary_data(op, bc_values, dst_owned, 3, op->side_stream);
-    hip_check(hipEventRecord(op->ev_join, op->side_stream), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(op->stream, op->ev_join, 0), "hipStreamWaitEvent");
-    if (bc_values) launch_boundary_data(op, bc_values, dst_owned, 4);
+    apply_with_faces(op, op->kind == GDM_OP_MASS, src_local, dst_owned, bc_values);
   } else {
     any_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned);
     if (bc_values) launch_boundary_data(op, bc_values, dst_owned);
@@ -1889,13 +1918,7 @@ int gdm_apply_bc_fn(gdm_op *op, const double *src_local, double *dst_owned, int 
   // interior launch's workgroups (one per CU, all of its LDS) to drain
   const double *bc = fill_stage_boundary(op, fn_kind, params, n_params, t_g, alpha, t_k, op->stream);
   if (op->concurrent && !op->mesh.periodic) {
-    hip_check(hipEventRecord(op->ev_fork, op->stream), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(op->side_stream, op->ev_fork, 0), "hipStreamWaitEvent");
-    hip_check(launch_stencil(op, false, src_local, dst_owned), "stencil launch");
-    if (bc) launch_boundary_data(op, bc, dst_owned, 3, op->side_stream);
-    hip_check(hipEventRecord(op->ev_join, op->side_stream), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(op->stream, op->ev_join, 0), "hipStreamWaitEvent");
-    if (bc) launch_boundary_data(op, bc, dst_owned, 4);
+    apply_with_faces(op, false, src_local, dst_owned, bc);
   } else {
     any_stencil(op, false, src_local, dst_owned);
     if (bc) launch_boundary_data(op, bc, dst_owned);

@@ -579,6 +579,217 @@ __global__ void __launch_bounds__(64 * (NP + NC), (64 * (NP + NC)) / 256) stenci
     consumer7<P, R, NC, NP, BK>(a, t);
 }
 
+// ---------------------------------------------------------------------------
+// Inflow boundary-data term (advection/stiffness.h:473-532 with a.n < 0):
+//   rhs(node) += |a.n| sum_{q on face} u+_q phi_node(x_q) JxW_q
+// factorised over the two tangential directions of the face:
+//   step 1: T[q1][i0] = sum_m U[q1][qs0(i0) + m] w0[i0][m]
+//   step 2: dst(i0, i1) += scale * sum_m w1[i1][m] T[qs1(i1) + m][i0]
+// Step 1 stages ROWS rows of U (the q-range of FACE_CHUNK consecutive nodes)
+// in LDS with coalesced loads; each lane then owns one node and reads its
+// weights node-minor (w0T), so every global access is a contiguous wave row.
+// ---------------------------------------------------------------------------
+// boundary values U(i0, i1) of the face ([Q1][Q0] array).  (Evaluating the
+// stage values of a built-in function here instead, per point, measured 2-3x
+// slower than reading them: each lane's six consecutive points make every
+// table read touch 64 cache lines; gdm_apply_bc_fn fills the array first.)
+struct BcArr {
+  const double *__restrict__ U;
+  int Q0;
+  __device__ __forceinline__ double operator()(int i0, int i1) const { return U[(int64_t)i1 * Q0 + i0]; }
+};
+
+
+template <int ROWS, class Src>
+__global__ void __launch_bounds__(FACE_CHUNK) face_step1_kernel(const Src U, int Q0, int Q1,
+                                                                 int i0_begin, int n0,
+                                                                 const int *__restrict__ qs0,
+                                                                 const double *__restrict__ w0T, int wmax0,
+                                                                 int ldw0, int qmax, double *__restrict__ T) {
+  extern __shared__ double sh[];  // [ROWS][qmax]
+  const int c0 = blockIdx.x * FACE_CHUNK;
+  const int q1b = blockIdx.y * ROWS;
+  const int nc = min(FACE_CHUNK, n0 - c0);
+  const int ia = i0_begin + c0;
+  const int qa = qs0[ia];
+  const int nq = min(Q0, qs0[ia + nc - 1] + wmax0) - qa;  // <= qmax (host-checked)
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    if (q1b + r < Q1) {
+      for (int e = threadIdx.x; e < nq; e += FACE_CHUNK) sh[r * qmax + e] = U(qa + e, q1b + r);
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x >= nc) return;
+  const int i0 = ia + threadIdx.x;
+  const int b = qs0[i0] - qa;
+  const int mend = min(wmax0, nq - b);  // weights past the node's own count are 0
+  double s[ROWS];
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) s[r] = 0.0;
+  for (int m = 0; m < mend; ++m) {
+    const double w = w0T[(int64_t)m * ldw0 + i0];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) s[r] = fma(w, sh[r * qmax + b + m], s[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r)
+    if (q1b + r < Q1) T[(int64_t)(q1b + r) * n0 + c0 + threadIdx.x] = s[r];
+}
+
+// Step 1 in cell form: for one row q1 of the face, every local cell c reduces
+// its p + 1 contiguous boundary values with its category's (p+1) x (p+1) table
+// (S_c[l] = sum_q Phi[cat(c)][l][q] U[q1][c (p+1) + q], one contiguous read per
+// cell, no per-node weight rows), then every owned node gathers the S_c of the
+// cells whose DoF boxes contain it (system.h:195-246 box offsets).
+__device__ __forceinline__ int face_category(int c, int p, int n) {
+  const int half = p / 2;
+  return c < half ? c : (c < n - half ? half : p + c - n);
+}
+__device__ __forceinline__ int face_box_offset(int c, int p, int n) {
+  const int half = p / 2;
+  return c < half ? 0 : min(n, c + half + 1) - p;
+}
+
+template <int P, class Src>
+__device__ __forceinline__ void face_cell_step1_body(const Src &U, int Q0, int Q1, int rpb, int i0_begin, int n0,
+                                                     const int *__restrict__ crange, const double *__restrict__ phi,
+                                                     int ncell_total, int cell_begin, double *__restrict__ T,
+                                                     int block) {
+  constexpr int N1 = P + 1;
+  extern __shared__ double sh[];  // [P][N1][N1] Phi, then [ncells][N1] S
+  double *sphi = sh, *S = sh + P * N1 * N1;
+  const int ncells = Q0 / N1;
+  for (int e = threadIdx.x; e < P * N1 * N1; e += blockDim.x) sphi[e] = phi[e];
+  const int r0 = block * rpb, r1 = min(Q1, r0 + rpb);
+  for (int row = r0; row < r1; ++row) {
+    __syncthreads();  // Phi ready / previous row's gather done
+    for (int c = threadIdx.x; c < ncells; c += blockDim.x) {
+      const int cat = face_category(cell_begin + c, P, ncell_total);
+      double v[N1];
+#pragma unroll
+      for (int q = 0; q < N1; ++q) v[q] = U(c * N1 + q, row);
+      const double *ph = sphi + cat * N1 * N1;
+#pragma unroll
+      for (int l = 0; l < N1; ++l) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < N1; ++q) s = fma(ph[l * N1 + q], v[q], s);
+        S[c * N1 + l] = s;
+      }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < n0; t += blockDim.x) {
+      const int i0 = i0_begin + t;
+      const int cf = crange[2 * i0], cl = crange[2 * i0 + 1];
+      double acc = 0.0;
+      for (int c = cf; c <= cl; ++c) acc += S[c * N1 + (i0 - face_box_offset(cell_begin + c, P, ncell_total))];
+      T[(int64_t)row * n0 + t] = acc;
+    }
+  }
+}
+
+// Step 1 of the rows [block rpb, block rpb + rpb) at once, all threads of the
+// workgroup (the stencil's tail): the rows (contiguous in U) are staged in LDS
+// with coalesced 16-B loads, all of them in flight together; each (row, cell)
+// reduction then reads its N1 values from LDS and writes its N1 results over
+// them (the same positions: in place, no barrier); one barrier; every
+// (row, node) gather.  The same sums in the same order as
+// face_cell_step1_body.  LDS: Phi, then [rpb][Q0] (U rows, then S).
+template <int P>
+__device__ __forceinline__ void face_cell_step1_rows(const BcArr &U, int Q0, int Q1, int rpb, int i0_begin, int n0,
+                                                     const int *__restrict__ crange, const double *__restrict__ phi,
+                                                     int ncell_total, int cell_begin, double *__restrict__ T,
+                                                     int block) {
+  constexpr int N1 = P + 1, MAXLD = 8;
+  extern __shared__ double sh[];
+  double *sphi = sh, *S = sh + ((P * N1 * N1 + 1) & ~1);  // 16-B aligned rows
+  const int ncells = Q0 / N1;
+  for (int e = threadIdx.x; e < P * N1 * N1; e += blockDim.x) sphi[e] = phi[e];
+  const int r0 = block * rpb, nr = min(Q1, r0 + rpb) - r0;
+  // stage rows r0 .. r0 + nr - 1 (nr * Q0 contiguous doubles of U)
+  const double *src = U.U + (int64_t)r0 * Q0;
+  const int n = nr * Q0;
+  if ((((uintptr_t)src) & 15) == 0 && (n & 1) == 0) {
+    const dpair *s2 = (const dpair *)src;
+    ldouble2 *d2 = (ldouble2 *)S;
+    for (int eb = 0; eb < n / 2; eb += MAXLD * (int)blockDim.x) {
+      dpair v[MAXLD];
+#pragma unroll
+      for (int k = 0; k < MAXLD; ++k) {
+        const int e = eb + k * (int)blockDim.x + (int)threadIdx.x;
+        if (e < n / 2) v[k] = __builtin_nontemporal_load(s2 + e);
+      }
+#pragma unroll
+      for (int k = 0; k < MAXLD; ++k) {
+        const int e = eb + k * (int)blockDim.x + (int)threadIdx.x;
+        if (e < n / 2) d2[e] = v[k];
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < n; e += blockDim.x) S[e] = src[e];
+  }
+  __syncthreads();  // Phi and the rows staged
+  for (int e = threadIdx.x; e < nr * ncells; e += blockDim.x) {
+    const int r = e / ncells, c = e - r * ncells;
+    double *Sc = S + (int64_t)r * Q0 + c * N1;
+    double v[N1];
+#pragma unroll
+    for (int q = 0; q < N1; ++q) v[q] = Sc[q];
+    const double *ph = sphi + face_category(cell_begin + c, P, ncell_total) * N1 * N1;
+#pragma unroll
+    for (int l = 0; l < N1; ++l) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < N1; ++q) acc = fma(ph[l * N1 + q], v[q], acc);
+      Sc[l] = acc;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < nr * n0; e += blockDim.x) {
+    const int r = e / n0, t = e - r * n0;
+    const int i0 = i0_begin + t;
+    const int cf = crange[2 * i0], cl = crange[2 * i0 + 1];
+    const double *Sr = S + (int64_t)r * Q0;
+    double acc = 0.0;
+    for (int c = cf; c <= cl; ++c) acc += Sr[c * N1 + (i0 - face_box_offset(cell_begin + c, P, ncell_total))];
+    T[(int64_t)(r0 + r) * n0 + t] = acc;
+  }
+}
+
+template <int P, class Src>
+__global__ void __launch_bounds__(512) face_cell_step1_kernel(const Src U, int Q0, int Q1, int rpb,
+                                                               int i0_begin, int n0, const int *__restrict__ crange,
+                                                               const double *__restrict__ phi, int ncell_total,
+                                                               int cell_begin, double *__restrict__ T) {
+  face_cell_step1_body<P>(U, Q0, Q1, rpb, i0_begin, n0, crange, phi, ncell_total, cell_begin, T, blockIdx.x);
+}
+
+// every inflow face's step 1 (cell form) in one launch, face = blockIdx.y:
+// the faces are independent (own T), so their rows share the GPU instead of
+// running one face after the other (gdmk_launch_faces_step1)
+template <class Src>
+struct Step1Face {
+  Src U;
+  int Q0, Q1, i0_begin, n0;
+  const int *crange;
+  const double *phi;
+  int ncell_total, cell_begin;
+  double *T;
+};
+template <class Src>
+struct Step1Set {
+  Step1Face<Src> f[BcStage::kMaxFaces];
+  int rpb;
+};
+template <int P, class Src>
+__global__ void __launch_bounds__(512) face_cell_step1_multi_kernel(const Step1Set<Src> set) {
+  const Step1Face<Src> &F = set.f[blockIdx.y];
+  if ((int)blockIdx.x * set.rpb >= F.Q1) return;
+  face_cell_step1_body<P>(F.U, F.Q0, F.Q1, set.rpb, F.i0_begin, F.n0, F.crange, F.phi, F.ncell_total, F.cell_begin,
+                          F.T, blockIdx.x);
+}
+
 // ===========================================================================
 // Fused Kronecker stencil, v8.  Same roles and tiles as v7:
 //   * each producer wave DMAs its own row groups of the (TY + 2p) x (64 + 2p)
@@ -653,7 +864,7 @@ struct Geom8 {
 };
 
 // LDS hand-off counters of the v8 stencil (indices into Tile7::sync)
-enum { SY_FULL = 0, SY_FREE = 2, SY_YWF = 4, SY_YWR = 5 };
+enum { SY_FULL = 0, SY_FREE = 2, SY_YWF = 4, SY_YWR = 5, SY_TAIL = 6 };
 
 // wait until counter c has reached target (wave-uniform).  One asm block,
 // spin included: a loop the compiler can see splits the live ranges of the
@@ -1165,6 +1376,14 @@ __device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
   GDM_LDS_BARRIER();  // tables in LDS, counters zeroed
+#ifdef GDM_X_STAGGER
+  if (GDM_X_STAGGER_SEL) {
+    for (int q = 0; q < GDM_X_STAGGER; ++q) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
+#ifdef GDM_X_PRIOHALF
+  if (t.cw >= NC / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   // Input plane zz scatters with its z column: a wall column for zz < W or
   // zz >= Nz - W (LDS table), else the interior one.  Blocks of W planes that
   // hold a wall column run the table path for all their planes, the others
@@ -1200,9 +1419,46 @@ __device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) 
   }
 }
 
+// Work the stencil's workgroups take on once their chunk is done: the inflow
+// faces' step 1 (face_cell_step1_body), row blocks handed out by a device
+// counter.  One workgroup per CU and one round: the wall tiles finish last,
+// and this fills their tail.  A separate side-stream launch of the same work
+// starved the stencil instead: its small workgroups took the CUs that the
+// stencil's whole-CU workgroups were waiting for.  The counter only grows:
+// this launch owns [base, base + items + gridDim), every workgroup ending with
+// one claim past the items.
+struct StencilTail {
+  Step1Set<BcArr> s1;
+  int nfaces, items;
+  int first[BcStage::kMaxFaces + 1];  // item range of face f: [first[f], first[f + 1])
+  unsigned long long *counter;
+  unsigned long long base;
+};
+
+template <int P>
+__device__ __forceinline__ void stencil_tail(const StencilTail &tl, lu32 *slot) {
+  __syncthreads();  // every role is done with the LDS
+  while (true) {
+    if (threadIdx.x == 0) {
+      const unsigned long long v = atomicAdd(tl.counter, 1ull) - tl.base;
+      *slot = (unsigned)(v < (unsigned long long)tl.items ? v : (unsigned long long)tl.items);
+    }
+    __syncthreads();
+    const int it = (int)*slot;
+    __syncthreads();
+    if (it >= tl.items) break;
+    int f = 0;
+    while (f + 1 < tl.nfaces && it >= tl.first[f + 1]) ++f;
+    const Step1Face<BcArr> &F = tl.s1.f[f];
+    face_cell_step1_rows<P>(F.U, F.Q0, F.Q1, tl.s1.rpb, F.i0_begin, F.n0, F.crange, F.phi, F.ncell_total,
+                            F.cell_begin, F.T, it - tl.first[f]);
+    __syncthreads();  // the rows' gathers are done with S before the next item's reductions
+  }
+}
+
 template <int P, int R, int NC, int NP, int BK, int CH, int PF>
 __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, NP, BK>::WGS) / 4)
-    stencil8_kernel(StencilArgs a) {
+    stencil8_kernel(StencilArgs a, StencilTail tail) {
   using G = Geom8<P, R, NC, NP, BK>;
   static_assert(G::lds_bytes() <= G::LDS_CAP, "LDS budget");
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1271,6 +1527,7 @@ __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, N
     producer8<P, R, NC, NP, BK, CH>(a, t);
   else
     consumer8<P, R, NC, NP, BK, PF>(a, t);
+  if (tail.items > 0) stencil_tail<P>(tail, t.sync + SY_TAIL);
 }
 
 // ---------------------------------------------------------------------------
@@ -1317,149 +1574,6 @@ __global__ void __launch_bounds__(256) chol_lines_kernel(double *__restrict__ v,
   }
 }
 
-// ---------------------------------------------------------------------------
-// Inflow boundary-data term (advection/stiffness.h:473-532 with a.n < 0):
-//   rhs(node) += |a.n| sum_{q on face} u+_q phi_node(x_q) JxW_q
-// factorised over the two tangential directions of the face:
-//   step 1: T[q1][i0] = sum_m U[q1][qs0(i0) + m] w0[i0][m]
-//   step 2: dst(i0, i1) += scale * sum_m w1[i1][m] T[qs1(i1) + m][i0]
-// Step 1 stages ROWS rows of U (the q-range of FACE_CHUNK consecutive nodes)
-// in LDS with coalesced loads; each lane then owns one node and reads its
-// weights node-minor (w0T), so every global access is a contiguous wave row.
-// ---------------------------------------------------------------------------
-// boundary values U(i0, i1) of the face ([Q1][Q0] array).  (Evaluating the
-// stage values of a built-in function here instead, per point, measured 2-3x
-// slower than reading them: each lane's six consecutive points make every
-// table read touch 64 cache lines; gdm_apply_bc_fn fills the array first.)
-struct BcArr {
-  const double *__restrict__ U;
-  int Q0;
-  __device__ __forceinline__ double operator()(int i0, int i1) const { return U[(int64_t)i1 * Q0 + i0]; }
-};
-
-
-template <int ROWS, class Src>
-__global__ void __launch_bounds__(FACE_CHUNK) face_step1_kernel(const Src U, int Q0, int Q1,
-                                                                 int i0_begin, int n0,
-                                                                 const int *__restrict__ qs0,
-                                                                 const double *__restrict__ w0T, int wmax0,
-                                                                 int ldw0, int qmax, double *__restrict__ T) {
-  extern __shared__ double sh[];  // [ROWS][qmax]
-  const int c0 = blockIdx.x * FACE_CHUNK;
-  const int q1b = blockIdx.y * ROWS;
-  const int nc = min(FACE_CHUNK, n0 - c0);
-  const int ia = i0_begin + c0;
-  const int qa = qs0[ia];
-  const int nq = min(Q0, qs0[ia + nc - 1] + wmax0) - qa;  // <= qmax (host-checked)
-#pragma unroll
-  for (int r = 0; r < ROWS; ++r) {
-    if (q1b + r < Q1) {
-      for (int e = threadIdx.x; e < nq; e += FACE_CHUNK) sh[r * qmax + e] = U(qa + e, q1b + r);
-    }
-  }
-  __syncthreads();
-  if ((int)threadIdx.x >= nc) return;
-  const int i0 = ia + threadIdx.x;
-  const int b = qs0[i0] - qa;
-  const int mend = min(wmax0, nq - b);  // weights past the node's own count are 0
-  double s[ROWS];
-#pragma unroll
-  for (int r = 0; r < ROWS; ++r) s[r] = 0.0;
-  for (int m = 0; m < mend; ++m) {
-    const double w = w0T[(int64_t)m * ldw0 + i0];
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) s[r] = fma(w, sh[r * qmax + b + m], s[r]);
-  }
-#pragma unroll
-  for (int r = 0; r < ROWS; ++r)
-    if (q1b + r < Q1) T[(int64_t)(q1b + r) * n0 + c0 + threadIdx.x] = s[r];
-}
-
-// Step 1 in cell form: for one row q1 of the face, every local cell c reduces
-// its p + 1 contiguous boundary values with its category's (p+1) x (p+1) table
-// (S_c[l] = sum_q Phi[cat(c)][l][q] U[q1][c (p+1) + q], one contiguous read per
-// cell, no per-node weight rows), then every owned node gathers the S_c of the
-// cells whose DoF boxes contain it (system.h:195-246 box offsets).
-__device__ __forceinline__ int face_category(int c, int p, int n) {
-  const int half = p / 2;
-  return c < half ? c : (c < n - half ? half : p + c - n);
-}
-__device__ __forceinline__ int face_box_offset(int c, int p, int n) {
-  const int half = p / 2;
-  return c < half ? 0 : min(n, c + half + 1) - p;
-}
-
-template <int P, class Src>
-__device__ __forceinline__ void face_cell_step1_body(const Src &U, int Q0, int Q1, int rpb, int i0_begin, int n0,
-                                                     const int *__restrict__ crange, const double *__restrict__ phi,
-                                                     int ncell_total, int cell_begin, double *__restrict__ T,
-                                                     int block) {
-  constexpr int N1 = P + 1;
-  extern __shared__ double sh[];  // [P][N1][N1] Phi, then [ncells][N1] S
-  double *sphi = sh, *S = sh + P * N1 * N1;
-  const int ncells = Q0 / N1;
-  for (int e = threadIdx.x; e < P * N1 * N1; e += blockDim.x) sphi[e] = phi[e];
-  const int r0 = block * rpb, r1 = min(Q1, r0 + rpb);
-  for (int row = r0; row < r1; ++row) {
-    __syncthreads();  // Phi ready / previous row's gather done
-    for (int c = threadIdx.x; c < ncells; c += blockDim.x) {
-      const int cat = face_category(cell_begin + c, P, ncell_total);
-      double v[N1];
-#pragma unroll
-      for (int q = 0; q < N1; ++q) v[q] = U(c * N1 + q, row);
-      const double *ph = sphi + cat * N1 * N1;
-#pragma unroll
-      for (int l = 0; l < N1; ++l) {
-        double s = 0.0;
-#pragma unroll
-        for (int q = 0; q < N1; ++q) s = fma(ph[l * N1 + q], v[q], s);
-        S[c * N1 + l] = s;
-      }
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < n0; t += blockDim.x) {
-      const int i0 = i0_begin + t;
-      const int cf = crange[2 * i0], cl = crange[2 * i0 + 1];
-      double acc = 0.0;
-      for (int c = cf; c <= cl; ++c) acc += S[c * N1 + (i0 - face_box_offset(cell_begin + c, P, ncell_total))];
-      T[(int64_t)row * n0 + t] = acc;
-    }
-  }
-}
-
-template <int P, class Src>
-__global__ void __launch_bounds__(512) face_cell_step1_kernel(const Src U, int Q0, int Q1, int rpb,
-                                                               int i0_begin, int n0, const int *__restrict__ crange,
-                                                               const double *__restrict__ phi, int ncell_total,
-                                                               int cell_begin, double *__restrict__ T) {
-  face_cell_step1_body<P>(U, Q0, Q1, rpb, i0_begin, n0, crange, phi, ncell_total, cell_begin, T, blockIdx.x);
-}
-
-// every inflow face's step 1 (cell form) in one launch, face = blockIdx.y:
-// the faces are independent (own T), so their rows share the GPU instead of
-// running one face after the other (gdmk_launch_faces_step1)
-template <class Src>
-struct Step1Face {
-  Src U;
-  int Q0, Q1, i0_begin, n0;
-  const int *crange;
-  const double *phi;
-  int ncell_total, cell_begin;
-  double *T;
-};
-template <class Src>
-struct Step1Set {
-  Step1Face<Src> f[BcStage::kMaxFaces];
-  int rpb;
-};
-template <int P, class Src>
-__global__ void __launch_bounds__(512) face_cell_step1_multi_kernel(const Step1Set<Src> set) {
-  const Step1Face<Src> &F = set.f[blockIdx.y];
-  if ((int)blockIdx.x * set.rpb >= F.Q1) return;
-  face_cell_step1_body<P>(F.U, F.Q0, F.Q1, set.rpb, F.i0_begin, F.n0, F.crange, F.phi, F.ncell_total, F.cell_begin,
-                          F.T, blockIdx.x);
-}
-
 // scale sum_m w1[i1][m] T[q + m][t], the product rounded on its own: the
 // compiler may not fuse it into the later add (one FMA would round
 // differently from the face-by-face path's dst + G)
@@ -1468,8 +1582,19 @@ __device__ __forceinline__ double face_step2_value(const double *__restrict__ T,
                                                    const double *__restrict__ w1, int wmax1, double scale) {
   const double *w = w1 + (int64_t)i1 * wmax1;
   const int n = qc1[i1], q = qs1[i1];
+  const double *Tc = T + (int64_t)q * n0 + t;
   double s = 0.0;
-  for (int m = 0; m < n; ++m) s = fma(w[m], T[(int64_t)(q + m) * n0 + t], s);
+  int m = 0;
+  // groups of 6 loads in flight, the FMAs in increasing m (the order of the
+  // one-at-a-time loop: same bits)
+  for (; m + 6 <= n; m += 6) {
+    double tv[6];
+#pragma unroll
+    for (int u = 0; u < 6; ++u) tv[u] = Tc[(int64_t)(m + u) * n0];
+#pragma unroll
+    for (int u = 0; u < 6; ++u) s = fma(w[m + u], tv[u], s);
+  }
+  for (; m < n; ++m) s = fma(w[m], Tc[(int64_t)m * n0], s);
   double v;
   {
 #pragma clang fp contract(off)
@@ -1518,27 +1643,86 @@ struct Step2AddSet {
   int n;
   int64_t N0, N1, own_off;
 };
-__global__ void __launch_bounds__(256) face_step2_add_kernel(const Step2AddSet set, double *__restrict__ dst) {
+// One thread per node column t and R1 consecutive i1 rows: the rows' T
+// windows overlap (consecutive nodes shift by one cell), so the thread walks
+// the union of their q ranges once and feeds each row's sum in increasing m
+// -- the same FMA sequence per node as face_step2_value, with ~R1 / 4 of its
+// T loads.  Weights and q ranges are wave-uniform (scalar loads).
+template <int R1>
+__global__ void __launch_bounds__(64) face_step2_add_kernel(const Step2AddSet set, double *__restrict__ dst) {
   const int f = blockIdx.z;
   const Step2Face &F = set.f[f];
   const FaceAddFace &A = set.g[f];
-  const int t = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y;
-  if (t >= F.n0 || F.i1_begin + r >= F.i1_end) return;
-  const int64_t o = A.base + (int64_t)t * A.stride0 + (int64_t)r * A.stride1;
-  const int64_t gi = o + set.own_off;
-  const int c[3] = {(int)(gi % set.N0), (int)((gi / set.N0) % set.N1), (int)(gi / (set.N0 * set.N1))};
-  for (int g = 0; g < f; ++g)
-    if (face_add_member(set.g[g], c)) return;
-  double v = dst[o];
-  v = v + face_step2_value(F.T, F.n0, t, F.i1_begin + r, F.qs1, F.qc1, F.w1, F.wmax1, F.scale);
-  for (int g = f + 1; g < set.n; ++g) {
-    const FaceAddFace &H = set.g[g];
-    if (!face_add_member(H, c)) continue;
-    const Step2Face &S = set.f[g];
-    const int u0 = H.a0 < 0 ? 0 : c[H.a0] - H.b0, u1 = H.a1 < 0 ? 0 : c[H.a1] - H.b1;
-    v = v + face_step2_value(S.T, S.n0, u0, S.i1_begin + u1, S.qs1, S.qc1, S.w1, S.wmax1, S.scale);
+  const int r0 = blockIdx.y * R1, nr = min(R1, F.i1_end - F.i1_begin - r0);
+  if (nr <= 0) return;
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  const bool on = t < F.n0;
+  const int tt = on ? t : F.n0 - 1;  // idle lanes repeat a valid column (no divergence in the q walk)
+  const int i1a = F.i1_begin + r0;
+  int qlo = F.qs1[i1a], qhi = qlo;
+#pragma unroll
+  for (int j = 0; j < R1; ++j)
+    if (j < nr) {
+      qlo = min(qlo, F.qs1[i1a + j]);
+      qhi = max(qhi, F.qs1[i1a + j] + F.qc1[i1a + j]);
+    }
+  double sum[R1];
+  int qs[R1], qe[R1];
+  const double *wr[R1];
+#pragma unroll
+  for (int j = 0; j < R1; ++j) {
+    sum[j] = 0.0;
+    qs[j] = j < nr ? F.qs1[i1a + j] : 0;
+    qe[j] = j < nr ? qs[j] + F.qc1[i1a + j] : 0;
+    wr[j] = F.w1 + (int64_t)(i1a + j) * F.wmax1 - qs[j];  // wr[j][q] = w1[i1][q - qs]
   }
-  dst[o] = v;
+  const double *Tc = F.T + tt;
+  int q = qlo;
+  for (; q + 6 <= qhi; q += 6) {
+    double tv[6];
+#pragma unroll
+    for (int u = 0; u < 6; ++u) tv[u] = Tc[(int64_t)(q + u) * F.n0];
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+#pragma unroll
+      for (int j = 0; j < R1; ++j)
+        if (q + u >= qs[j] && q + u < qe[j]) sum[j] = fma(wr[j][q + u], tv[u], sum[j]);
+  }
+  for (; q < qhi; ++q) {
+    const double tv = Tc[(int64_t)q * F.n0];
+#pragma unroll
+    for (int j = 0; j < R1; ++j)
+      if (q >= qs[j] && q < qe[j]) sum[j] = fma(wr[j][q], tv, sum[j]);
+  }
+  if (!on) return;
+#pragma unroll
+  for (int j = 0; j < R1; ++j) {
+    if (j >= nr) break;
+    const int r = r0 + j;
+    const int64_t o = A.base + (int64_t)t * A.stride0 + (int64_t)r * A.stride1;
+    const int64_t gi = o + set.own_off;
+    const int c[3] = {(int)(gi % set.N0), (int)((gi / set.N0) % set.N1), (int)(gi / (set.N0 * set.N1))};
+    bool mine = true;
+    for (int g = 0; g < f; ++g)
+      if (face_add_member(set.g[g], c)) mine = false;
+    if (!mine) continue;  // the node's first face adds every face's term
+    double gv;
+    {
+#pragma clang fp contract(off)
+      gv = F.scale * sum[j];
+    }
+    asm volatile("" : "+v"(gv));
+    double v = dst[o];
+    v = v + gv;
+    for (int g = f + 1; g < set.n; ++g) {
+      const FaceAddFace &H = set.g[g];
+      if (!face_add_member(H, c)) continue;
+      const Step2Face &S = set.f[g];
+      const int u0 = H.a0 < 0 ? 0 : c[H.a0] - H.b0, u1 = H.a1 < 0 ? 0 : c[H.a1] - H.b1;
+      v = v + face_step2_value(S.T, S.n0, u0, S.i1_begin + u1, S.qs1, S.qc1, S.w1, S.wmax1, S.scale);
+    }
+    dst[o] = v;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1627,8 +1811,47 @@ static hipError_t launch7_p(int bk, const StencilArgs &a, hipStream_t st) {
   }
 }
 
+// what the caller asks of a launch's tail (gdmk_launch_stencil8)
+struct TailReq {
+  const FaceArgs *faces;
+  int n;
+  unsigned long long *counter, base, *claims;
+};
+
+// the tail work of a launch: step 1 of the faces fa[0, nf) (cell form, each its
+// own T); items = 0 when nf = 0 or a face cannot run in the tail
+static StencilTail make_tail(const FaceArgs *fa, int nf, int p, unsigned long long *counter,
+                             unsigned long long base, size_t lds_avail) {
+  StencilTail tl{};
+  if (nf <= 0 || nf > BcStage::kMaxFaces || !counter) return tl;
+  // rows per item: as many as the launch's LDS holds (the rows form keeps
+  // them all), at most 4
+  size_t q0max = 1;
+  for (int i = 0; i < nf; ++i) q0max = std::max(q0max, (size_t)std::max(fa[i].Q0, 1));
+  const size_t phi = sizeof(double) * (size_t)((p * (p + 1) * (p + 1) + 1) & ~1);
+  if (lds_avail <= phi) return tl;
+  tl.s1.rpb = (int)std::min<size_t>(4, (lds_avail - phi) / (sizeof(double) * q0max));
+  if (tl.s1.rpb < 1) return StencilTail{};
+  int items = 0;
+  for (int i = 0; i < nf; ++i) {
+    const FaceArgs &f = fa[i];
+    const size_t need = sizeof(double) * ((size_t)f.p * (f.p + 1) * (f.p + 1) + (size_t)tl.s1.rpb * f.Q0);
+    if (!f.phi0 || f.p != p || !f.T || f.Q1 <= 0 || f.i0_end <= f.i0_begin || need > lds_avail) return StencilTail{};
+    tl.s1.f[i] = Step1Face<BcArr>{BcArr{f.U, f.Q0}, f.Q0, f.Q1, f.i0_begin, f.i0_end - f.i0_begin, f.crange0, f.phi0,
+                                  f.ncell0_total, f.cell0_begin, f.T};
+    tl.first[i] = items;
+    items += (f.Q1 + tl.s1.rpb - 1) / tl.s1.rpb;
+  }
+  tl.first[nf] = items;
+  tl.nfaces = nf;
+  tl.items = items;
+  tl.counter = counter;
+  tl.base = base;
+  return tl;
+}
+
 template <int P, int R, int NC, int NP, int BK, int CH, int PF>
-static hipError_t launch8_t(const StencilArgs &a, hipStream_t st) {
+static hipError_t launch8_t(const StencilArgs &a, const TailReq &tr, hipStream_t st) {
   using G = Geom8<P, R, NC, NP, BK>;
   static_assert(G::lds_bytes() <= 160 * 1024, "LDS budget");
   const size_t lds = G::lds_bytes();
@@ -1643,20 +1866,28 @@ static hipError_t launch8_t(const StencilArgs &a, hipStream_t st) {
     if (a.cz1[r] > a.cz0[r]) nz += (a.cz1[r] - a.cz0[r] + a.zchunk - 1) / a.zchunk;
   dim3 grid((a.Nx + G::TX - 1) / G::TX, (a.out_y1 - a.out_y0 + G::TY - 1) / G::TY, nz);
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return hipSuccess;
-  hipLaunchKernelGGL((stencil8_kernel<P, R, NC, NP, BK, CH, PF>), grid, dim3(G::NT), lds, st, a);
-  return hipGetLastError();
+  const StencilTail tail = make_tail(tr.faces, tr.n, P, tr.counter, tr.base, lds);
+  hipLaunchKernelGGL((stencil8_kernel<P, R, NC, NP, BK, CH, PF>), grid, dim3(G::NT), lds, st, a, tail);
+  const hipError_t e = hipGetLastError();
+  // counter claims of this launch: every item once, and one past the end per workgroup
+  if (e == hipSuccess && tail.items > 0)
+    *tr.claims = (unsigned long long)tail.items + (unsigned long long)grid.x * grid.y * grid.z;
+  return e;
 }
 
 template <int P, int R, int NC, int NP, int PF>
-static hipError_t launch8_p(int bk, const StencilArgs &a, hipStream_t st) {
+static hipError_t launch8_p(int bk, const StencilArgs &a, const TailReq &tail, hipStream_t st) {
   const bool vec = (a.Nx % 2 == 0) && ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0);
   switch (bk) {
 #ifdef GDM_ONLY_ADV16  // fast experiment builds: advection, 16-B DMA only
-    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF>(a, st) : hipErrorInvalidValue;
+    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF>(a, tail, st) : hipErrorInvalidValue;
 #else
-    case 0: return vec ? launch8_t<P, R, NC, NP, 0, 16, PF>(a, st) : launch8_t<P, R, NC, NP, 0, 4, PF>(a, st);
-    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF>(a, st) : launch8_t<P, R, NC, NP, 1, 4, PF>(a, st);
-    case 2: return vec ? launch8_t<P, R, NC, NP, 2, 16, PF>(a, st) : launch8_t<P, R, NC, NP, 2, 4, PF>(a, st);
+    case 0:
+      return vec ? launch8_t<P, R, NC, NP, 0, 16, PF>(a, tail, st) : launch8_t<P, R, NC, NP, 0, 4, PF>(a, tail, st);
+    case 1:
+      return vec ? launch8_t<P, R, NC, NP, 1, 16, PF>(a, tail, st) : launch8_t<P, R, NC, NP, 1, 4, PF>(a, tail, st);
+    case 2:
+      return vec ? launch8_t<P, R, NC, NP, 2, 16, PF>(a, tail, st) : launch8_t<P, R, NC, NP, 2, 4, PF>(a, tail, st);
 #endif
     default: return hipErrorInvalidValue;
   }
@@ -1664,27 +1895,32 @@ static hipError_t launch8_p(int bk, const StencilArgs &a, hipStream_t st) {
 
 }  // namespace gdmk
 
-extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, const gdmk::StencilArgs &a, hipStream_t st) {
+extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, const gdmk::StencilArgs &a, const gdmk::FaceArgs *tail_faces,
+                                           int n_tail, unsigned long long *counter, unsigned long long base,
+                                           unsigned long long *claims, hipStream_t st) {
   using namespace gdmk;
+  *claims = 0;
+  const TailReq tail{tail_faces, n_tail, counter, base, claims};
+  hipError_t e = hipErrorInvalidValue;
   switch (p) {
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 1
-    case 1: return launch8_p<1, 4, 8, 8, 3>(bk, a, st);
+    case 1: e = launch8_p<1, 4, 8, 8, 3>(bk, a, tail, st); break;
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 3
-    case 3: return launch8_p<3, 4, 8, 8, 3>(bk, a, st);
+    case 3: e = launch8_p<3, 4, 8, 8, 3>(bk, a, tail, st); break;
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 5
-    case 5: return launch8_p<5, GDM_R5, GDM_NC5, GDM_NP5, GDM_PF5>(bk, a, st);
+    case 5: e = launch8_p<5, GDM_R5, GDM_NC5, GDM_NP5, GDM_PF5>(bk, a, tail, st); break;
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 7
-    case 7: return launch8_p<7, GDM_R7, GDM_NC7, GDM_NP7, GDM_PF7>(bk, a, st);
+    case 7: e = launch8_p<7, GDM_R7, GDM_NC7, GDM_NP7, GDM_PF7>(bk, a, tail, st); break;
 #endif
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 9
-    case 9: return launch8_p<9, 2, 8, 8, 3>(bk, a, st);
+    case 9: e = launch8_p<9, 2, 8, 8, 3>(bk, a, tail, st); break;
 #endif
-    
-    default: return hipErrorInvalidValue;
+    default: break;
   }
+  return e;
 }
 
 // <P, R, NC, NP>: R output rows per consumer wave, NC consumer and NP producer
@@ -1846,6 +2082,9 @@ extern "C" hipError_t gdmk_launch_faces_step2_add(const gdmk::FaceArgs *fa, cons
                                                   int64_t N0, int64_t N1, int64_t own_off, double *dst,
                                                   hipStream_t st) {
   using namespace gdmk;
+  // rows per thread: 1 / 2 / 4 / 8 measured 41.5 / 37.0 / 45.6 / 74.9 us at C3
+  // (three 512^2 faces, profiles/r5_experiments/face_step2_rows.txt)
+  constexpr int kRows = 2;
   if (n <= 0) return hipSuccess;
   if (n > BcStage::kMaxFaces || N0 <= 0 || N1 <= 0) return hipErrorNotSupported;
   Step2AddSet set{};
@@ -1860,11 +2099,11 @@ extern "C" hipError_t gdmk_launch_faces_step2_add(const gdmk::FaceArgs *fa, cons
     if (!f.T || fg[i].e0 - fg[i].b0 != n0 || fg[i].e1 - fg[i].b1 != f.i1_end - f.i1_begin) return hipErrorNotSupported;
     set.f[i] = Step2Face{f.T, n0, f.i1_begin, f.i1_end, f.qs1, f.qc1, f.w1, f.wmax1, f.scale};
     set.g[i] = fg[i];
-    gx = std::max(gx, (n0 + 255) / 256);
-    gy = std::max(gy, f.i1_end - f.i1_begin);
+    gx = std::max(gx, (n0 + 63) / 64);
+    gy = std::max(gy, (f.i1_end - f.i1_begin + kRows - 1) / kRows);
   }
   if (gx <= 0 || gy <= 0) return hipSuccess;
-  hipLaunchKernelGGL(face_step2_add_kernel, dim3(gx, gy, n), dim3(256), 0, st, set, dst);
+  hipLaunchKernelGGL(face_step2_add_kernel<kRows>, dim3(gx, gy, n), dim3(64), 0, st, set, dst);
   return hipGetLastError();
 }
 
