@@ -676,7 +676,8 @@ void build_faces(gdm_op *op) {
 // tail / n_tail: inflow faces whose step 1 the stencil's workgroups run once
 // their chunk is done (v8 only); *tail_done reports whether it ran
 hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst, int zb = -1, int ze = -1,
-                          const gdmk::FaceArgs *tail = nullptr, int n_tail = 0, bool *tail_done = nullptr) {
+                          const gdmk::FaceArgs *tail = nullptr, int n_tail = 0, bool *tail_done = nullptr,
+                          int zb2 = 0, int ze2 = 0) {
   if (tail_done) *tail_done = false;
   const gdm_layout &L = op->layout;
   gdmk::StencilArgs a{};
@@ -751,10 +752,14 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
   // one round of workgroups on 256 CUs (two rounds measured 0.93 vs 0.85 ms
   // at C3, 0.27 vs 0.22 ms at C4: profiles/r3g/variants.txt)
   const int64_t chunks = std::max<int64_t>(1, (256 * wgs + tiles - 1) / tiles);
-  const int len = ze - zb;
-  a.cz0[0] = zb; a.cz1[0] = ze; a.cz0[1] = a.cz1[1] = 0;
+  // a second range (gdm_apply_planes2), clipped to the owned planes like the first
+  zb2 = std::max(zb2, a.out_z0);
+  ze2 = std::min(ze2, a.out_z1);
+  const int len2 = std::max(0, ze2 - zb2);
+  const int len = ze - zb + len2;
+  a.cz0[0] = zb; a.cz1[0] = ze; a.cz0[1] = len2 ? zb2 : 0; a.cz1[1] = len2 ? ze2 : 0;
   a.zchunk = (int)std::max<int64_t>(std::min(len, 8), (len + chunks - 1) / chunks);
-  a.nchunk0 = (len + a.zchunk - 1) / a.zchunk;
+  a.nchunk0 = (ze - zb + a.zchunk - 1) / a.zchunk;
   const bool with_tail = n_tail > 0 && tail && op->tail_counter;
   unsigned long long claims = 0;
   const hipError_t e = gdmk_launch_stencil8(op->p, bk, a, with_tail ? tail : nullptr, with_tail ? n_tail : 0,
@@ -1493,6 +1498,36 @@ int gdm_apply_planes(gdm_op *op, const double *src_local, double *dst_owned, int
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, plane_begin, plane_end),
+            "stencil launch");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
+int gdm_apply_planes2(gdm_op *op, const double *src_local, double *dst_owned, int b0, int e0, int b1, int e1) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
+  if (op->part_axis != 2) return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_planes2: plane ranges need a 3D mesh");
+  if (op->mesh.periodic) return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_planes2: periodic constraints");
+  if (e0 > b0 && e1 > b1 && b1 < e0 && b0 < e1) return fail(GDM_ERR_ARG, "gdm_apply_planes2: overlapping ranges");
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  if (e0 <= b0) {  // one range: the plain launch
+    hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, b1, e1), "stencil launch");
+    return GDM_OK;
+  }
+  if (e1 <= b1) {
+    hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, b0, e0), "stencil launch");
+    return GDM_OK;
+  }
+  // the v7 path (small meshes) takes one range per launch
+  int ty8 = 32, wgs8 = 1;
+  gdmk_stencil8_geom(op->p, &ty8, &wgs8);
+  if (!(op->K[1] >= ty8 + 2 * op->p + 2 && op->K[0] >= 64 + 2 * op->p + 2)) {
+    hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, b0, e0), "stencil launch");
+    hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, b1, e1), "stencil launch");
+    return GDM_OK;
+  }
+  hip_check(launch_stencil(op, op->kind == GDM_OP_MASS, src_local, dst_owned, b0, e0, nullptr, 0, nullptr, b1, e1),
             "stencil launch");
   return GDM_OK;
   GDM_GUARD_END

@@ -128,6 +128,7 @@ def load():
         "gdm_apply": [P, P, P, P],
         "gdm_add_boundary_data": [P, P, P],
         "gdm_apply_planes": [P, P, P, i32, i32],
+        "gdm_apply_planes2": [P, P, P, i32, i32, i32, i32],
         "gdm_mass_apply": [P, P, P],
         "gdm_mass_solve": [P, P, P],
         "gdm_mass_solve_rk": [P, P, d, P, P, d, P, P],

@@ -285,11 +285,9 @@ def apply_overlapped(op, halo, src_local, dst_owned, bc_values=None):
         halo.finish(reqs)
     if hi <= lo:
         op.apply_planes(src_local, dst_owned, pb, pe)
-    else:
-        if lo > pb:
-            op.apply_planes(src_local, dst_owned, pb, lo)
-        if pe > hi:
-            op.apply_planes(src_local, dst_owned, hi, pe)
+    elif lo > pb or pe > hi:
+        # both edge ranges in one launch (gdm_apply_planes2)
+        op.apply_planes2(src_local, dst_owned, pb, lo, hi, pe)
     if bc_values is not None:
         op.add_boundary_data(bc_values, dst_owned)
     return dst_owned

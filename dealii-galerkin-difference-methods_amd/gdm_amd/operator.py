@@ -130,6 +130,13 @@ class GdmOperator:
               "gdm_apply_planes")
         return dst_owned
 
+    def apply_planes2(self, src_local, dst_owned, b0, e0, b1, e1):
+        """apply_planes of two plane ranges in one launch (gdm_apply_planes2)"""
+        self._check_sizes(src_local, dst_owned)
+        check(self.lib.gdm_apply_planes2(self.h, _ptr(src_local), _ptr(dst_owned), int(b0), int(e0), int(b1),
+                                         int(e1)), "gdm_apply_planes2")
+        return dst_owned
+
     def add_boundary_data(self, bc_values, dst_owned):
         self._check_sizes(None, dst_owned)
         check(self.lib.gdm_add_boundary_data(self.h, _ptr(bc_values), _ptr(dst_owned)), "gdm_add_boundary_data")

@@ -318,8 +318,8 @@ class StiffnessMatrixOperator {
     if (hi <= lo) {
       check(gdm_apply_planes(op, u, dst, pb, pe), "gdm_apply_planes");
     } else {
-      if (lo > pb) check(gdm_apply_planes(op, u, dst, pb, lo), "gdm_apply_planes");
-      if (pe > hi) check(gdm_apply_planes(op, u, dst, hi, pe), "gdm_apply_planes");
+      // both edge ranges in one launch
+      if (lo > pb || pe > hi) check(gdm_apply_planes2(op, u, dst, pb, lo, hi, pe), "gdm_apply_planes2");
     }
   }
 

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 12
+#define GDM_HIP_ABI_VERSION 13
 
 enum gdm_status {
   GDM_OK = 0,
@@ -187,6 +187,11 @@ int gdm_apply(gdm_op *op, const double *src_local, double *dst_owned, const doub
  * (the overlap of update_ghost_values, advection/stiffness.h:343, with the cell
  * loop).  Boundary data: gdm_add_boundary_data afterwards. */
 int gdm_apply_planes(gdm_op *op, const double *src_local, double *dst_owned, int plane_begin, int plane_end);
+/* gdm_apply_planes of two plane ranges [b0, e0) and [b1, e1) in ONE launch
+ * (ABI 13): the p planes next to both slab edges after the exchange, so the
+ * thin edge ranges share the GPU instead of running one after the other.  The
+ * same bits as two gdm_apply_planes calls.  An empty range is allowed. */
+int gdm_apply_planes2(gdm_op *op, const double *src_local, double *dst_owned, int b0, int e0, int b1, int e1);
 /* dst_owned += inflow boundary-data term only (the bc part of gdm_apply,
  * advection/stiffness.h:520-529 with a.n < 0); no-op for other kinds */
 int gdm_add_boundary_data(gdm_op *op, const double *bc_values, double *dst_owned);

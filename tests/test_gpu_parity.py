@@ -401,3 +401,27 @@ def test_apply_planes_overlap_split(n_ranks, rank):
     y2.fill_(7.0)
     apply_overlapped(op, None, src, y2, bc)
     assert rel(host(y2), host(y1)) < 1e-14
+
+
+@pytest.mark.parametrize("p,kind", [(5, "advection"), (7, "wave")])
+def test_apply_planes2_equals_two_range_launches(p, kind):
+    """gdm_apply_planes2 (both slab-edge ranges in one launch, ABI 13) gives
+    the bits of two gdm_apply_planes calls; overlapping ranges are refused."""
+    g = _gdm()
+    shape = (100, 70, 64)
+    params = (0.7, -0.4, 0.3) if kind == "advection" else ()
+    op = g.GdmOperator(3, p, shape, 0.0, 1.0, kind, params=params, rank=1, n_ranks=3)
+    L = op.layout
+    pb, pe = L["owned_plane_begin"], L["owned_plane_end"]
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    src = torch.rand(op.n_local, dtype=torch.float64, device="cuda", generator=gen)
+    y1, y2 = op.new_vector(local=False), op.new_vector(local=False)
+    y1.fill_(3.0)
+    y2.fill_(3.0)
+    op.apply_planes(src, y1, pb, pb + p)
+    op.apply_planes(src, y1, pe - p, pe)
+    op.apply_planes2(src, y2, pb, pb + p, pe - p, pe)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    with pytest.raises(g.GdmError, match="overlapping"):
+        op.apply_planes2(src, y2, pb, pb + 2 * p, pb + p, pe)
