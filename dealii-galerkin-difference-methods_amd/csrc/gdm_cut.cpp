@@ -261,14 +261,18 @@ struct PolyGen {
   const std::vector<double> &qx, &qw;
   std::vector<QPoint> &inside;
   std::vector<SPoint> &surface;
+  std::vector<QPoint> *outside;  // f > 0 (q_partitioning.positive), NULL: not collected
   int n_splits = 0;
 
-  void tensor(const double lo[2], const double hi[2]) {
+  void tensor(const double lo[2], const double hi[2], std::vector<QPoint> *dst) {
+    if (!dst) return;
     const double L0 = hi[0] - lo[0], L1 = hi[1] - lo[1];
     for (size_t b = 0; b < qx.size(); ++b)
       for (size_t a = 0; a < qx.size(); ++a)
-        inside.push_back({lo[0] + L0 * qx[a], lo[1] + L1 * qx[b], qw[a] * qw[b] * L0 * L1});
+        dst->push_back({lo[0] + L0 * qx[a], lo[1] + L1 * qx[b], qw[a] * qw[b] * L0 * L1});
   }
+  // the region a point of level-set value fv belongs to (exact zeros: neither)
+  std::vector<QPoint> *region(double fv) { return fv < 0.0 ? &inside : (fv > 0.0 ? outside : nullptr); }
 
   void generate(const double lo[2], const double hi[2], int n_box_splits) {
     const double c[2] = {0.5 * (lo[0] + hi[0]), 0.5 * (lo[1] + hi[1])};
@@ -285,9 +289,12 @@ struct PolyGen {
         vmin = std::min(vmin, fv);
         vmax = std::max(vmax, fv);
       }
-    if (vmin > kLimit) return;
+    if (vmin > kLimit) {
+      tensor(lo, hi, outside);
+      return;
+    }
     if (vmax < -kLimit) {
-      tensor(lo, hi);
+      tensor(lo, hi, &inside);
       return;
     }
     double low[2];
@@ -308,8 +315,8 @@ struct PolyGen {
       lr[d] = mid;
       generate(lo, hl, n_box_splits + 1);
       generate(lr, hi, n_box_splits + 1);
-    } else if (f.value(c[0], c[1]) < 0.0) {  // midpoint rule
-      inside.push_back({c[0], c[1], 4.0 * dx[0] * dx[1]});
+    } else if (auto *dst = region(f.value(c[0], c[1]))) {  // midpoint rule
+      dst->push_back({c[0], c[1], 4.0 * dx[0] * dx[1]});
     }
   }
 
@@ -352,13 +359,15 @@ struct PolyGen {
       const double sb = f.value(s, t);
       at(a + 0.5 * L, h_hi, s, t);
       const double st = f.value(s, t);
-      if (sb > 0.0 && st > 0.0) continue;
+      const bool definite = (sb < 0.0 && st < 0.0) || (sb > 0.0 && st > 0.0);
+      if (definite && sb > 0.0 && !outside) continue;
       for (int k = 0; k < nq; ++k) {
         const double cc = a + L * qx[k], wc = qw[k] * L;
-        if (sb < 0.0 && st < 0.0) {
+        if (definite) {
+          std::vector<QPoint> &dst = sb < 0.0 ? inside : *outside;
           for (int m = 0; m < nq; ++m) {
             at(cc, h_lo + Lh * qx[m], s, t);
-            inside.push_back({s, t, wc * qw[m] * Lh});
+            dst.push_back({s, t, wc * qw[m] * Lh});
           }
           continue;
         }
@@ -370,10 +379,10 @@ struct PolyGen {
           const double nxt = r < hr.size() ? hr[r] : h_hi, Ls = nxt - prev;
           if (Ls > 0.0) {
             at(cc, prev + 0.5 * Ls, s, t);
-            if (f.value(s, t) < 0.0)
+            if (auto *dst = region(f.value(s, t)))
               for (int m = 0; m < nq; ++m) {
                 at(cc, prev + Ls * qx[m], s, t);
-                inside.push_back({s, t, wc * qw[m] * Ls});
+                dst->push_back({s, t, wc * qw[m] * Ls});
               }
           }
           prev = nxt;
@@ -484,10 +493,12 @@ int bernstein_location(int dim, int k, const double *vals, const std::vector<dou
 }
 
 void saye_poly(const TensorPoly &f, const std::vector<double> &qx, const std::vector<double> &qw,
-               std::vector<QPoint> &inside, std::vector<SPoint> &surface, int *n_splits) {
+               std::vector<QPoint> &inside, std::vector<SPoint> &surface, int *n_splits,
+               std::vector<QPoint> *outside) {
   inside.clear();
   surface.clear();
-  PolyGen gen{f, qx, qw, inside, surface};
+  if (outside) outside->clear();
+  PolyGen gen{f, qx, qw, inside, surface, outside};
   const double lo[2] = {0.0, 0.0}, hi[2] = {1.0, 1.0};
   gen.generate(lo, hi, 0);
   if (n_splits) *n_splits += gen.n_splits;

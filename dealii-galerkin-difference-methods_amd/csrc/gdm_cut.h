@@ -58,9 +58,11 @@ std::vector<double> gauss_lobatto(int n);
 int bernstein_location(int dim, int k, const double *vals, const std::vector<double> &support);
 
 // QuadratureGenerator<2> (Saye) for a FE_Q(k) cell level set on the unit box,
-// with deal.II's box splits / midpoint fallback; *n_splits counts splits
+// with deal.II's box splits / midpoint fallback; *n_splits counts splits;
+// outside (when given) receives the f > 0 region's quadrature of the same pass
 void saye_poly(const TensorPoly &f, const std::vector<double> &qx, const std::vector<double> &qw,
-               std::vector<QPoint> &inside, std::vector<SPoint> &surface, int *n_splits);
+               std::vector<QPoint> &inside, std::vector<SPoint> &surface, int *n_splits,
+               std::vector<QPoint> *outside = nullptr);
 
 struct Shapes {
   // values / reference derivatives of the p+1 1D shapes at a point

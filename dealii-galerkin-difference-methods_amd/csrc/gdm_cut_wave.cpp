@@ -1,8 +1,9 @@
 // gdm_cut_wave.cpp -- host assembly of the cut-cell parts of the wave /
-// heat / poisson application (applications/wave, location "inside", no domain
-// Dirichlet data: wave-app.cc presets "wave", "heat-rk", "heat-impl" at
-// dim = 1 and 2, "step85" at dim = 2) for the device operator of gdm_capi.cpp
-// ("Cut-cell wave" in include/gdm_hip.h).
+// heat / poisson application (applications/wave: wave-app.cc presets "wave",
+// "heat-rk", "heat-impl" (inside field, interface data), "heat-composite",
+// "wave-composite" (inside + outside fields, domain data, interface coupling)
+// at dim = 1 and 2, "step85" at dim = 2) for the device operator of
+// gdm_capi.cpp ("Cut-cell wave" in include/gdm_hip.h).
 //
 // The mesh is a GDM line [left, right] or square [left, right]^2 cut by the
 // FE_Q(k) interpolant of a level set (wave/discretization.h:78-93:
@@ -345,9 +346,16 @@ void assemble1d(gdm_cut_wave_system &S, const double *ls_values) {
 
 // dim = 2: cells (cx, cy) lexicographic, DoF (ix, iy) -> ix + N iy; the
 // caller's level-set values per cell at the (k+1)^2 Gauss-Lobatto points
-// (a along x fastest); quadrature by saye_poly (gdm_cut.cpp)
+// (a along x fastest); quadrature by saye_poly (gdm_cut.cpp), the region of
+// S.location from the same pass.  Field, data and coupling terms as in
+// assemble1d: interface data on the surface points (normal flipped for
+// OUTSIDE), domain data on the boundary faces in the region (QGauss(p+1) on
+// the face, outward normal; the face's location from the Bernstein
+// coefficients of the level set on it -- an intersected boundary face is
+// refused), the composite coupling on the surface points of intersected cells.
 void assemble2d(gdm_cut_wave_system &S, const double *ls_values) {
   const int p = S.p, n = S.n, k = S.k, n1 = p + 1, nd = n1 * n1, nk = (k + 1) * (k + 1);
+  const int loc_f = S.location, inv = -loc_f;
   const int64_t N = n + 1, NN = N * N;
   const double h = S.h;
   std::vector<double> gx, gw;
@@ -356,18 +364,23 @@ void assemble2d(gdm_cut_wave_system &S, const double *ls_values) {
   S.loc.assign((size_t)n * n, OUTSIDE);
   std::vector<std::vector<QPoint>> cq((size_t)n * n);
   std::vector<std::vector<SPoint>> cs((size_t)n * n);
+  std::vector<QPoint> other;
   for (int cy = 0; cy < n; ++cy)
     for (int cx = 0; cx < n; ++cx) {
       const size_t c = (size_t)cy * n + cx;
       const double *vals = ls_values + c * nk;
       S.loc[c] = (int8_t)bernstein_location(2, k, vals, gl);
-      if (S.loc[c] == INSIDE) {
+      if (S.loc[c] == loc_f) {
         for (int b = 0; b < n1; ++b)
           for (int a = 0; a < n1; ++a) cq[c].push_back({gx[a], gx[b], gw[a] * gw[b]});
       } else if (S.loc[c] == INTERSECTED) {
         TensorPoly f;
         f.interpolate(k, vals, gl);
-        saye_poly(f, gx, gw, cq[c], cs[c], &S.n_splits);
+        if (loc_f == INSIDE) {
+          saye_poly(f, gx, gw, cq[c], cs[c], &S.n_splits);
+        } else {
+          saye_poly(f, gx, gw, other, cs[c], &S.n_splits, &cq[c]);
+        }
       }
     }
   for (int8_t l : S.loc) ++S.cells[l == INSIDE ? 0 : (l == INTERSECTED ? 1 : 2)];
@@ -381,18 +394,19 @@ void assemble2d(gdm_cut_wave_system &S, const double *ls_values) {
   int64_t d[100], e[100];
   for (int cy = 0; cy < n; ++cy)
     for (int cx = 0; cx < n; ++cx)
-      if (S.loc[(size_t)cy * n + cx] != INSIDE) {
+      if (S.loc[(size_t)cy * n + cx] != loc_f) {
         dofs(cx, cy, d);
         for (int i = 0; i < nd; ++i) full_row[(size_t)d[i]] = 1;
       }
   for (int64_t r = 0; r < NN; ++r)
     if (full_row[(size_t)r]) S.zero_rows.push_back(r);
-  Slots C, M, K;
+  Slots C, M, K, X;
   C.init(2, N, p + 1);
   M.init(2, N, p + 1);
   K.init(2, N, p + 1);
+  X.init(2, N, p + 1);
   std::vector<Trip> ff, fg, ev;
-  std::vector<double> val(nd), grx(nd), gry(nd);
+  std::vector<double> val(nd), grx(nd), gry(nd), dn(nd);
   auto eval = [&](int cx, int cy, double s, double t) {
     Shapes sx, sy;
     shapes_1d(p, cat_of(cx), s, sx);
@@ -405,11 +419,31 @@ void assemble2d(gdm_cut_wave_system &S, const double *ls_values) {
         gry[i] = sx.v[ix] * sy.d[iy] / h;
       }
   };
-  const double gd = S.nitsche / h;
+  const double gd = S.nitsche / h, tau = 0.5 * S.nitsche / h;
+  // Nitsche terms of one Dirichlet point (after eval; normal (nx, ny), weight
+  // jxw at global (xg, yg)): -(-d_n v u - d_n u v + gamma_D / h v u) into C, +
+  // into K, the data (gamma_D / h v - d_n v) into column si of Fg
+  auto dirichlet_point = [&](double nx, double ny, double jxw, double xg, double yg) {
+    const int64_t si = (int64_t)S.sx.size() / 2;
+    S.sx.push_back(xg);
+    S.sx.push_back(yg);
+    S.sn.push_back(nx);
+    S.sn.push_back(ny);
+    for (int i = 0; i < nd; ++i) dn[i] = grx[i] * nx + gry[i] * ny;
+    for (int i = 0; i < nd; ++i) {
+      fg.push_back({d[i], si, (gd * val[i] - dn[i]) * jxw});
+      for (int j = 0; j < nd; ++j) {
+        const double a = (-dn[i] * val[j] - val[i] * dn[j] + gd * val[i] * val[j]) * jxw;
+        C.add(d[i], d[j], -a);
+        K.add(d[i], d[j], a);
+      }
+    }
+  };
+  const double sg = loc_f == INSIDE ? 1.0 : -1.0;
   for (int cy = 0; cy < n; ++cy)
     for (int cx = 0; cx < n; ++cx) {
       const size_t c = (size_t)cy * n + cx;
-      if (S.loc[c] == OUTSIDE) continue;
+      if (S.loc[c] == inv) continue;
       dofs(cx, cy, d);
       const double x0 = S.lo + cx * h, y0 = S.lo + cy * h;
       for (const QPoint &q : cq[c]) {
@@ -431,40 +465,62 @@ void assemble2d(gdm_cut_wave_system &S, const double *ls_values) {
           }
         }
       }
-      for (const SPoint &sp : cs[c]) {
-        eval(cx, cy, sp.s, sp.t);
-        const double jxw = sp.w * h;
-        const int64_t si = (int64_t)S.sx.size() / 2;
-        S.sx.push_back(x0 + sp.s * h);
-        S.sx.push_back(y0 + sp.t * h);
-        S.sn.push_back(sp.nx);
-        S.sn.push_back(sp.ny);
-        for (int i = 0; i < nd; ++i) {
-          const double dni = grx[i] * sp.nx + gry[i] * sp.ny;
-          fg.push_back({d[i], si, (gd * val[i] - dni) * jxw});
-          for (int j = 0; j < nd; ++j) {
-            const double dnj = grx[j] * sp.nx + gry[j] * sp.ny;
-            const double a = (-dni * val[j] - val[i] * dnj + gd * val[i] * val[j]) * jxw;
-            C.add(d[i], d[j], -a);
-            K.add(d[i], d[j], a);
+      if (S.dirichlet & 1)
+        for (const SPoint &sp : cs[c]) {
+          eval(cx, cy, sp.s, sp.t);
+          dirichlet_point(sg * sp.nx, sg * sp.ny, sp.w * h, x0 + sp.s * h, y0 + sp.t * h);
+        }
+      if (S.dirichlet & 2)
+        for (int f = 0; f < 4; ++f) {
+          const int axis = f / 2, side = f % 2;
+          if ((axis == 0 ? cx : cy) != (side == 0 ? 0 : n - 1)) continue;
+          // the level set on the face: the support points with s (axis 0) or t (axis 1) = side
+          const double *vals = ls_values + c * nk;
+          double line[10];
+          for (int a = 0; a <= k; ++a)
+            line[a] = axis == 0 ? vals[(side ? k : 0) + (k + 1) * a] : vals[a + (k + 1) * (side ? k : 0)];
+          const int where = bernstein_location(1, k, line, gl);
+          if (where == INTERSECTED)
+            throw std::invalid_argument("cut_wave: the level set crosses a domain boundary face (not supported)");
+          if (where != loc_f) continue;
+          const double nv = 2.0 * side - 1.0;
+          for (int q = 0; q < n1; ++q) {
+            const double s = axis == 0 ? (double)side : gx[q], t = axis == 0 ? gx[q] : (double)side;
+            eval(cx, cy, s, t);
+            dirichlet_point(axis == 0 ? nv : 0.0, axis == 0 ? 0.0 : nv, gw[q] * h, x0 + s * h, y0 + t * h);
           }
         }
-      }
+      if (S.coupled)
+        for (const SPoint &sp : cs[c]) {
+          // r_own -= (-0.5 d_n v [u] -+ v n.{grad u} +- tau v [u]), [u] = u_in - u_out,
+          // {grad u} = (grad u_in + grad u_out) / 2, n the level-set normal
+          eval(cx, cy, sp.s, sp.t);
+          const double jxw = sp.w * h;
+          for (int i = 0; i < nd; ++i) dn[i] = grx[i] * sp.nx + gry[i] * sp.ny;
+          for (int i = 0; i < nd; ++i)
+            for (int j = 0; j < nd; ++j) {
+              const double vdn = dn[i] * val[j], vnd = val[i] * dn[j], vv = val[i] * val[j];
+              const double a_in = (-0.5 * vdn - sg * 0.5 * vnd + sg * tau * vv) * jxw;
+              const double a_out = (0.5 * vdn - sg * 0.5 * vnd - sg * tau * vv) * jxw;
+              C.add(d[i], d[j], -(loc_f == INSIDE ? a_in : a_out));
+              X.add(d[i], d[j], -(loc_f == INSIDE ? a_out : a_in));
+            }
+        }
     }
   // ghost penalty faces (mass.h:86-105, stiffness.h:80-98, 330-395): QGauss(p+1)
-  // on every face of a non-outside cell to a neighbour where one of the two is
-  // intersected and the other not outside, visited from both cells
+  // on every face of a cell not of location inv to a neighbour where one of the
+  // two is intersected and the other not of location inv, visited from both cells
   std::map<int64_t, std::vector<double>> jump;
   for (int cy = 0; cy < n; ++cy)
     for (int cx = 0; cx < n; ++cx) {
       const int lc = S.loc[(size_t)cy * n + cx];
-      if (lc == OUTSIDE) continue;
+      if (lc == inv) continue;
       for (int f = 0; f < 4; ++f) {
         const int axis = f / 2, side = f % 2;
         const int nx = cx + (axis == 0 ? 2 * side - 1 : 0), ny = cy + (axis == 1 ? 2 * side - 1 : 0);
         if (nx < 0 || nx >= n || ny < 0 || ny >= n) continue;
         const int ln = S.loc[(size_t)ny * n + nx];
-        if (!((lc == INTERSECTED && ln != OUTSIDE) || (ln == INTERSECTED && lc != OUTSIDE))) continue;
+        if (!((lc == INTERSECTED && ln != inv) || (ln == INTERSECTED && lc != inv))) continue;
         jump.clear();
         dofs(cx, cy, d);
         dofs(nx, ny, e);
@@ -498,10 +554,10 @@ void assemble2d(gdm_cut_wave_system &S, const double *ls_values) {
   C.csr(S.c_rp, S.c_ci, S.c_v, false);
   M.csr(S.m_rp, S.m_ci, S.m_v, true);
   K.csr(S.s_rp, S.s_ci, S.s_v, true);
+  X.csr(S.x_rp, S.x_ci, S.x_v, false);
   triplets_csr(ff, NN, S.ff_rp, S.ff_ci, S.ff_v);
   triplets_csr(fg, NN, S.fg_rp, S.fg_ci, S.fg_v);
   triplets_csr(ev, (int64_t)S.qw.size(), S.e_rp, S.e_ci, S.e_v);
-  S.x_rp.assign((size_t)NN + 1, 0);  // no coupling in 2D
 }
 
 }  // namespace
@@ -521,8 +577,6 @@ int gdmh_cut_wave_create(int dim, int p, int n_sub, double lo, double hi, int ls
   try {
     if ((location != INSIDE && location != OUTSIDE) || (flags & ~7))
       throw std::invalid_argument("cut_wave: location must be -1 (inside) or 1 (outside), flags in bits 0-2");
-    if (dim == 2 && (location != INSIDE || flags != 1))
-      throw std::invalid_argument("cut_wave: dim 2 supports the inside field with interface data only");
     if (!out || !ls_values || (dim != 1 && dim != 2) || p < 1 || p > 9 || p % 2 == 0 || n_sub < p || !(hi > lo) ||
         ls_degree < 1 || ls_degree > 9)
       throw std::invalid_argument(

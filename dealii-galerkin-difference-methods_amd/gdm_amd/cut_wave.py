@@ -1,8 +1,9 @@
 """The cut-cell wave / heat / poisson application on the device (SURVEY §8
 f1): the reference's applications/wave at dim = 1 and 2 -- a GDM line or
-square cut by the FE_Q(k) interpolant of a level set, location "inside", no
-domain Dirichlet data -- through the C ABI "Cut-cell wave" entry points of
-include/gdm_hip.h.
+square cut by the FE_Q(k) interpolant of a level set; the inside field with
+interface data, or the composite pair (inside + outside fields, domain
+Dirichlet data, interface coupling) -- through the C ABI "Cut-cell wave"
+entry points of include/gdm_hip.h.
 
   CutWave            StiffnessMatrixOperator::compute_rhs
                      (wave/stiffness.h:42-407) = uncut 1D wave stencil of
@@ -16,8 +17,11 @@ include/gdm_hip.h.
                      u <- (M + dt K)^-1 (M u + dt F(t + dt))) and poisson
                      (u = K^-1 F, problem.h:46-71), with the postprocess
                      table (counter, t, L2, L1, Linf) of problem.h:504-615
-  preset(name, dim)  wave-app.cc:13-347: "wave", "heat-rk", "heat-impl"
-                     (dim 1, 2) and "step85" (dim 2)
+  preset(name, dim)  wave-app.cc:13-347: "wave", "heat-rk", "heat-impl",
+                     "heat-composite", "wave-composite" (dim 1, 2) and
+                     "step85" (dim 2)
+  CutWaveCompositeProblem  the composite presets (problem.h:128-214,
+                     :346-433): two handles coupled by gdm_cut_wave_couple
 
 f, g and the exact solution are the caller's functions of (x, t) in 1D and
 (x, y, t) in 2D (the reference's Function::value calls), evaluated on the
@@ -182,7 +186,8 @@ class CutWave:
 
 
 def preset(name, dim=1):
-    """wave-app.cc parameter sets (:13-57 step85, :62-150 heat, :215-262 wave):
+    """wave-app.cc parameter sets (:13-57 step85, :62-150 heat, :152-221
+    heat-composite, :222-285 wave, :286-347 wave-composite):
     FE degree 3, 40 cells per direction on [-1.21, 1.21], SignedDistance::Sphere
     of radius 1 in FE_Q(3), gamma_D = 5 p."""
     if dim == 1:
@@ -213,15 +218,16 @@ def preset(name, dim=1):
         cfl, cfl_pow = (0.3 / 9.0, 2.0) if name == "heat-rk" else (0.3, 1.0)
         return dict(base, gamma_M=0.75, gamma_A=1.5, f=f, g=ex, exact=ex, start_t=0.0, end_t=0.1, cfl=cfl,
                     cfl_pow=cfl_pow)
-    if name in ("heat-composite", "wave-composite") and dim == 1:
-        P = preset("heat-rk" if name == "heat-composite" else "wave", 1)
+    if name in ("heat-composite", "wave-composite"):
+        # wave-app.cc:152-221 / :286-347: the heat-rk / wave settings, the data on the domain boundary
+        P = preset("heat-rk" if name == "heat-composite" else "wave", dim)
         return dict(P, simulation=name, g_domain=P["g"], g=None)
     if name == "step85" and dim == 2:
         ex = lambda x, y, t: 1.0 - (x * x + y * y - 1.0)  # noqa: E731  1 - 2/dim (|x|^2 - 1)
         return dict(base, simulation="poisson", gamma_M=-1.0, gamma_A=0.5, f=lambda x, y, t: np.full_like(x, 4.0),
                     g=lambda x, y, t: np.ones_like(x), exact=ex, start_t=0.0, end_t=0.1, cfl=0.3, cfl_pow=1.0)
-    raise GdmError("cut_wave.preset: %r at dim %d (wave, heat-rk, heat-impl; heat-composite, wave-composite at "
-                   "dim 1; step85 at dim 2)" % (name, dim))
+    raise GdmError("cut_wave.preset: %r at dim %d (wave, heat-rk, heat-impl, heat-composite, wave-composite; "
+                   "step85 at dim 2)" % (name, dim))
 
 
 class CutWaveProblem:
@@ -339,7 +345,7 @@ class CutWaveProblem:
 
 
 class CutWaveCompositeProblem:
-    """WaveProblem<1>::run for the composite presets (wave/problem.h:128-214
+    """WaveProblem<dim>::run (dim 1, 2) for the composite presets (wave/problem.h:128-214
     heat-rk, :346-433 wave-rk): an inside and an outside field, one CutWave
     handle each (domain Dirichlet data + interface coupling), RK4 over the
     blocks (u_in, u_out) or (u_in, u_out, v_in, v_out) on the device; the
@@ -353,7 +359,7 @@ class CutWaveCompositeProblem:
         flags = CutWave.DOMAIN_DATA | CutWave.COUPLED
         self.f = [CutWave(P["p"], P["n"], P["left"], P["right"], P["level_set"], ghost_parameter_M=P["gamma_M"],
                           ghost_parameter_A=P["gamma_A"], nitsche=P["nitsche"], device=device, location=loc,
-                          flags=flags) for loc in (CutWave.INSIDE, CutWave.OUTSIDE)]
+                          flags=flags, dim=P.get("dim", 1)) for loc in (CutWave.INSIDE, CutWave.OUTSIDE)]
         self.wave = P["simulation"] == "wave-composite"
         self._fq = [cw.new_vector(max(cw.n_quad, 1)) for cw in self.f]
         self._gd = [cw.new_vector(max(cw.n_surface, 1)) for cw in self.f]

@@ -527,9 +527,9 @@ int gdm_cut_advection_create2(int fe_degree, int n_subdivisions, double left, do
 int gdm_cut_advection_couple(gdm_cut_advection *c, const double *u_partner, double *rhs);
 
 /* ------------------------------------------------------------------------
- * Cut-cell wave / heat / poisson (applications/wave, location
- * inside, no domain Dirichlet data, dim 1 and 2: the "wave", "heat-rk",
- * "heat-impl" and "step85" presets of wave-app.cc): the device operators of
+ * Cut-cell wave / heat / poisson (applications/wave, dim 1 and
+ * 2: the "wave", "heat-rk", "heat-impl", "heat-composite", "wave-composite"
+ * and "step85" presets of wave-app.cc): the device operators of
  * the reference's wave application on a GDM line / square cut by the FE_Q(k)
  * interpolant of a level set (WaveProblem<dim>, wave/problem.h).
  *
@@ -566,7 +566,7 @@ int gdm_cut_advection_couple(gdm_cut_advection *c, const double *u_partner, doub
  * lexicographic (x fastest).  Vectors: device pointers (n_dofs, n_quad,
  * n_surface doubles).
  *
- * Composite presets (heat-composite, wave-composite; dim 1): one handle per
+ * Composite presets (heat-composite, wave-composite; dim 1 and 2): one handle per
  * field, location GDM_CUT_INSIDE (phi < 0) or GDM_CUT_OUTSIDE (phi > 0), each
  * with its region's quadrature, mass and ghost-penalty faces (an intersected
  * cell and a neighbour not of the other location); flags select the Nitsche
@@ -575,8 +575,10 @@ int gdm_cut_advection_couple(gdm_cut_advection *c, const double *u_partner, doub
  * in the region, stiffness.h:262-330) and GDM_CUT_WAVE_COUPLED (the interface
  * terms of compute_rhs(BlockVector), stiffness.h:420-575: the own field's
  * part in compute_rhs, the partner's added by gdm_cut_wave_couple(c,
- * u_partner, rhs)).  The data points of gdm_cut_wave_points (sx, sn) are the
- * interface points followed by the domain faces, as selected.
+ * u_partner, rhs)).  The data points of gdm_cut_wave_points (sx, sn) are, cell
+ * by cell, the interface points followed by the Gauss points of the cell's
+ * domain faces (QGauss(p + 1) per face in 2D, outward normal), as selected.
+ * A domain boundary face the level set crosses is refused (2D).
  * ------------------------------------------------------------------------ */
 typedef struct gdm_cut_wave gdm_cut_wave;
 #define GDM_CUT_INSIDE (-1)

@@ -168,20 +168,23 @@ def _unique_sorted(roots):
 
 class QGen:
     """QuadratureGenerator<2> for one TensorPoly on a box in reference
-    coordinates: inside [(s, t, w)], surface [(s, t, w, normal)]."""
+    coordinates: inside [(s, t, w)] (f < 0), outside [(s, t, w)] (f > 0),
+    surface [(s, t, w, normal)]; deal.II fills q_partitioning.negative /
+    .positive in the same pass, a point whose level set is exactly 0 goes to
+    neither."""
 
     def __init__(self, f, qx, qw, tie=0):
         self.f, self.qx, self.qw, self.tie = f, qx, qw, tie
-        self.inside, self.surface = [], []
+        self.inside, self.outside, self.surface = [], [], []
         self.n_splits = 0
         self.n_midpoint = 0
         self.n_ties = 0
 
-    def _tensor(self, lo, hi):
+    def _tensor(self, lo, hi, dst):
         L0, L1 = hi[0] - lo[0], hi[1] - lo[1]
         for b, wb in zip(self.qx, self.qw):
             for a, wa in zip(self.qx, self.qw):
-                self.inside.append((lo[0] + L0 * a, lo[1] + L1 * b, wa * wb * L0 * L1))
+                dst.append((lo[0] + L0 * a, lo[1] + L1 * b, wa * wb * L0 * L1))
 
     def _restriction(self, hdir, hval):
         """the level set on the line x_hdir = hval as a function of the other coordinate"""
@@ -203,9 +206,10 @@ class QGen:
                 fv = f.value(vs, vt)
                 vmin, vmax = min(vmin, fv), max(vmax, fv)
         if vmin > LIMIT:
+            self._tensor(lo, hi, self.outside)
             return
         if vmax < -LIMIT:
-            self._tensor(lo, hi)
+            self._tensor(lo, hi, self.inside)
             return
         low = []
         for i in range(2):
@@ -229,8 +233,9 @@ class QGen:
             self.generate(tuple(lo_r), hi, n_box_splits + 1)
         else:
             self.n_midpoint += 1
-            if f.value(*c) < 0.0:
-                self.inside.append((c[0], c[1], (hi[0] - lo[0]) * (hi[1] - lo[1])))
+            fc = f.value(*c)
+            if fc != 0.0:
+                (self.inside if fc < 0.0 else self.outside).append((c[0], c[1], (hi[0] - lo[0]) * (hi[1] - lo[1])))
 
     def _height(self, hdir, lo, hi):
         f = self.f
@@ -252,13 +257,12 @@ class QGen:
                 continue
             m = 0.5 * (a + b)
             sb, st = bottom[0](m), top[0](m)
-            if sb > 0.0 and st > 0.0:
-                continue
             for x, w in zip(self.qx, self.qw):
                 cc, wc = a + L * x, w * L
-                if sb < 0.0 and st < 0.0:
+                if (sb < 0.0 and st < 0.0) or (sb > 0.0 and st > 0.0):
+                    dst = self.inside if sb < 0.0 else self.outside
                     for y, wy in zip(self.qx, self.qw):
-                        self.inside.append(point(cc, h_lo + Lh * y) + (wc * wy * Lh,))
+                        dst.append(point(cc, h_lo + Lh * y) + (wc * wy * Lh,))
                     continue
                 line = (lambda hh, cc=cc: f.value(*point(cc, hh)),
                         lambda hh, cc=cc: f.grad(*point(cc, hh))[hdir],
@@ -269,9 +273,11 @@ class QGen:
                     Ls = hb - ha
                     if not Ls > 0.0:
                         continue
-                    if f.value(*point(cc, 0.5 * (ha + hb))) < 0.0:
+                    fm = f.value(*point(cc, 0.5 * (ha + hb)))
+                    if fm != 0.0:
+                        dst = self.inside if fm < 0.0 else self.outside
                         for y, wy in zip(self.qx, self.qw):
-                            self.inside.append(point(cc, ha + Ls * y) + (wc * wy * Ls,))
+                            dst.append(point(cc, ha + Ls * y) + (wc * wy * Ls,))
                 if len(hr) == 1:
                     s, t = point(cc, hr[0])
                     gr = f.grad(s, t)
@@ -320,7 +326,7 @@ class CutWave2D:
                         self.ties.append((cx, cy))
                     self.n_splits += q.n_splits
                     self.n_midpoint += q.n_midpoint
-                    self.quad[(cx, cy)] = (q.inside, q.surface)
+                    self.quad[(cx, cy)] = (q.inside, q.surface, q.outside)
 
     # -- GDM indexing (system.h:195-246, 404-424) --------------------------
     def category(self, c):
@@ -354,34 +360,60 @@ class CutWave2D:
         gy = (dy[:, None, :] * vx[None, :, :]).reshape(-1, vx.shape[1])
         return val, np.stack([gx, gy])
 
-    def cell_quadrature(self, cx, cy):
-        """inside [(s, t, JxW)], surface [(s, t, JxW, normal)]"""
+    def cell_quadrature(self, cx, cy, location=INSIDE):
+        """the region's quadrature [(s, t, JxW)] and the surface [(s, t, JxW,
+        level-set normal)] of one cell"""
         loc, h = self.loc[cy, cx], self.h
-        if loc == OUTSIDE:
+        if loc == -location:
             return [], []
-        if loc == INSIDE:
+        if loc == location:
             return [(a, b, wa * wb * h * h) for b, wb in zip(self.qx, self.qw) for a, wa in zip(self.qx, self.qw)], []
-        ins, sur = self.quad[(cx, cy)]
-        return [(s, t, w * h * h) for s, t, w in ins], [(s, t, w * h, nn) for s, t, w, nn in sur]
+        ins, sur, out = self.quad[(cx, cy)]
+        reg = ins if location == INSIDE else out
+        return [(s, t, w * h * h) for s, t, w in reg], [(s, t, w * h, nn) for s, t, w, nn in sur]
+
+    def boundary_faces(self, cx, cy, location):
+        """(axis, side) of the cell's faces on the domain boundary that lie in
+        the region of `location` (NonMatching::FEInterfaceValues on the face:
+        MeshClassifier's face location, the Bernstein coefficients of the
+        level set restricted to the face)"""
+        n, k, out = self.n, self.k, []
+        T = lagrange_to_bernstein(self.gl)
+        for axis, side in ((0, 0), (0, 1), (1, 0), (1, 1)):
+            c = (cx, cy)[axis]
+            if c != (0 if side == 0 else n - 1):
+                continue
+            v = self.ls_values[cy, cx]  # [b (t), a (s)]
+            line = v[:, 0 if side == 0 else k] if axis == 0 else v[0 if side == 0 else k, :]
+            bern = T @ line
+            if bern.max() < 0.0:
+                where = INSIDE
+            elif bern.min() > 0.0:
+                where = OUTSIDE
+            else:
+                raise NotImplementedError("intersected domain boundary face (the level set crosses the box)")
+            if where == location:
+                out.append((axis, side))
+        return out
 
     def real_point(self, cx, cy, s, t):
         return self.xv[cx] + np.asarray(s) * self.h, self.xv[cy] + np.asarray(t) * self.h
 
     # -- ghost-penalty faces (mass.h:86-105 / stiffness.h:80-98) ------------
-    def gp_faces(self):
-        """(cell, neighbour, axis, side) per visit; each qualifying face is
-        visited from both cells"""
-        n, out = self.n, []
+    def gp_faces(self, location=INSIDE):
+        """(cell, neighbour, axis, side) per visit for the field of
+        `location`; each qualifying face is visited from both cells"""
+        n, out, inv = self.n, [], -location
         for cy in range(n):
             for cx in range(n):
                 a = self.loc[cy, cx]
-                if a == OUTSIDE:
+                if a == inv:
                     continue
                 for f, (nx, ny) in enumerate(((cx - 1, cy), (cx + 1, cy), (cx, cy - 1), (cx, cy + 1))):
                     if not (0 <= nx < n and 0 <= ny < n):
                         continue
                     b = self.loc[ny, nx]
-                    if (a == INTERSECTED and b != OUTSIDE) or (b == INTERSECTED and a != OUTSIDE):
+                    if (a == INTERSECTED and b != inv) or (b == INTERSECTED and a != inv):
                         out.append(((cx, cy), (nx, ny), f // 2, f % 2))
         return out
 
@@ -398,24 +430,44 @@ class CutWave2D:
         return idx, np.concatenate([gc[axis], -gn[axis]]), self.qw * self.h
 
     # -- operators ------------------------------------------------------------
-    def matrices(self, gamma_M, gamma_A, nitsche):
-        """mass M (None if gamma_M < 0), stiffness K, impl operator A
-        (compute_rhs(u) = -A u + data), load pieces: Ff [N, nq_in] (JxW
-        folded), Fg [N, n_surf]; evaluation E [nq_in, N]; the inside and
-        surface points"""
+    def matrices(self, gamma_M, gamma_A, nitsche, location=INSIDE, interface_data=True, domain_data=False,
+                 coupled=False):
+        """the field of `location`: mass M (None if gamma_M < 0), stiffness K,
+        impl operator A (compute_rhs(u) = -A u + data), load pieces Ff
+        [N, nq] (JxW folded), Fg [N, n_data] (the Dirichlet data points: the
+        surface points with interface_data (II, stiffness.h:205-259, normal
+        flipped for the outside field), the Gauss points of the boundary
+        faces in the region with domain_data (IV, :262-330)); with coupled the
+        composite interface terms of compute_rhs(BlockVector) (:420-575): the
+        own field's part in A, the partner's rhs contribution X (r += X
+        u_other); evaluation E [nq, N]; the region's and data points"""
         p, h, N2 = self.p, self.h, self.N * self.N
-        Mt, Kt, At, fft, fgt, et = [], [], [], [], [], []
+        Mt, Kt, At, Xt, fft, fgt, et = [], [], [], [], [], [], []
         qpts, spts = [], []
+        sg = 1.0 if location == INSIDE else -1.0
+        tau = 0.5 * nitsche / h
 
         def add(T, rows, cols, V):
             T.append((np.repeat(rows, len(cols)), np.tile(cols, len(rows)), V.reshape(-1)))
 
+        def nitsche_points(d, val, dn, w, pts):
+            """Dirichlet Nitsche terms at points with normal derivatives dn"""
+            S = (np.einsum("iq,jq,q->ij", -dn, val, w) + np.einsum("iq,jq,q->ij", val, -dn, w) +
+                 nitsche / h * np.einsum("iq,jq,q->ij", val, val, w))
+            add(Kt, d, d, S)
+            add(At, d, d, S)
+            s0 = len(spts)
+            spts.extend(pts)
+            si = np.arange(s0, s0 + len(pts))
+            for a in range(len(d)):
+                fgt.append((np.full(len(si), d[a]), si, (nitsche / h * val[a] - dn[a]) * w))
+
         for cy in range(self.n):
             for cx in range(self.n):
-                if self.loc[cy, cx] == OUTSIDE:
+                if self.loc[cy, cx] == -location:
                     continue
                 d = self.dofs(cx, cy)
-                ins, sur = self.cell_quadrature(cx, cy)
+                ins, sur = self.cell_quadrature(cx, cy, location)
                 if ins:
                     s = np.array([x[0] for x in ins])
                     t = np.array([x[1] for x in ins])
@@ -432,24 +484,40 @@ class CutWave2D:
                     for a in range(len(d)):
                         fft.append((np.full(len(qi), d[a]), qi, val[a] * w))
                         et.append((qi, np.full(len(qi), d[a]), val[a]))
-                if sur:
+                if sur and interface_data:
                     s = np.array([x[0] for x in sur])
                     t = np.array([x[1] for x in sur])
                     w = np.array([x[2] for x in sur])
-                    nrm = np.array([x[3] for x in sur]).T
+                    nrm = sg * np.array([x[3] for x in sur]).T
+                    val, grad = self.shapes(cx, cy, s, t)
+                    x, y = self.real_point(cx, cy, s, t)
+                    nitsche_points(d, val, np.einsum("diq,dq->iq", grad, nrm), w, list(zip(x, y, nrm[0], nrm[1])))
+                if domain_data:
+                    for axis, side in self.boundary_faces(cx, cy, location):
+                        q = self.qx
+                        s, t = (np.full(q.size, float(side)), q) if axis == 0 else (q, np.full(q.size, float(side)))
+                        val, grad = self.shapes(cx, cy, s, t)
+                        nv = 2.0 * side - 1.0
+                        x, y = self.real_point(cx, cy, s, t)
+                        nx_, ny_ = (nv, 0.0) if axis == 0 else (0.0, nv)
+                        nitsche_points(d, val, nv * grad[axis], self.qw * h,
+                                       [(a_, b_, nx_, ny_) for a_, b_ in zip(x, y)])
+                if sur and coupled:
+                    s = np.array([x[0] for x in sur])
+                    t = np.array([x[1] for x in sur])
+                    w = np.array([x[2] for x in sur])
+                    nrm = np.array([x[3] for x in sur]).T  # the level-set normal (outward of the inside)
                     val, grad = self.shapes(cx, cy, s, t)
                     dn = np.einsum("diq,dq->iq", grad, nrm)
-                    S = (np.einsum("iq,jq,q->ij", -dn, val, w) + np.einsum("iq,jq,q->ij", val, -dn, w) +
-                         nitsche / h * np.einsum("iq,jq,q->ij", val, val, w))
-                    add(Kt, d, d, S)
-                    add(At, d, d, S)
-                    s0 = len(spts)
-                    x, y = self.real_point(cx, cy, s, t)
-                    spts += list(zip(x, y, nrm[0], nrm[1]))
-                    si = np.arange(s0, s0 + len(sur))
-                    for a in range(len(d)):
-                        fgt.append((np.full(len(si), d[a]), si, (nitsche / h * val[a] - dn[a]) * w))
-        for c, nb, axis, side in self.gp_faces():
+                    # r_own -= (-0.5 dn_v [u] -+ v n.{grad u} +- tau v [u]), [u] = u_in - u_out
+                    VdN = np.einsum("iq,jq,q->ij", dn, val, w)
+                    VnD = np.einsum("iq,jq,q->ij", val, dn, w)
+                    VV = np.einsum("iq,jq,q->ij", val, val, w)
+                    a_in = -0.5 * VdN - sg * 0.5 * VnD + sg * tau * VV
+                    a_out = 0.5 * VdN - sg * 0.5 * VnD - sg * tau * VV
+                    add(At, d, d, a_in if location == INSIDE else a_out)
+                    add(Xt, d, d, -(a_out if location == INSIDE else a_in))
+        for c, nb, axis, side in self.gp_faces(location):
             idx, j, w = self._face_jump(c, nb, axis, side)
             J = np.einsum("iq,jq,q->ij", j, j, w)
             if gamma_M >= 0:
@@ -469,8 +537,9 @@ class CutWave2D:
 
         nq, ns = len(qpts), len(spts)
         return dict(M=build(Mt, (N2, N2), True) if gamma_M >= 0 else None, K=build(Kt, (N2, N2), True),
-                    A=build(At, (N2, N2), False), Ff=build(fft, (N2, nq), False), Fg=build(fgt, (N2, ns), False),
-                    E=build(et, (nq, N2), False), q=np.array(qpts).reshape(-1, 3), s=np.array(spts).reshape(-1, 4))
+                    A=build(At, (N2, N2), False), X=build(Xt, (N2, N2), False), Ff=build(fft, (N2, nq), False),
+                    Fg=build(fgt, (N2, ns), False), E=build(et, (nq, N2), False), q=np.array(qpts).reshape(-1, 3),
+                    s=np.array(spts).reshape(-1, 4))
 
     def interpolate(self, fun, t):
         """GDM::VectorTools::interpolate: vertex values (x fastest)"""
@@ -533,5 +602,80 @@ def run(simulation, max_steps=None, model=None):
         y = rk4_step(f, t0, h, y)
         n += 1
         rows.append((n, t0 + h) + m.errors(ops, y[:N], P["exact"], t0 + h))
+        time.advance()
+    return rows, m, ops
+
+
+# -- composite presets (wave-app.cc:152-221 heat-composite, :286-347 wave-composite, dim = 2) --
+def composite_params(kind):
+    """an inside and an outside field coupled across the circle, domain
+    Dirichlet data on the box faces (all in the outside region), no
+    interface data; heat-composite on the heat-rk settings, wave-composite on
+    the wave settings"""
+    if kind == "heat-composite":
+        ex = lambda x, y, t: x ** 9 * y ** 8 * math.exp(-t)  # noqa: E731
+        f = lambda x, y, t: -x ** 7 * y ** 6 * math.exp(-t) * (x * x * y * y + 72 * y * y + 56 * x * x)  # noqa: E731
+        return dict(p=3, n=40, left=-1.21, right=1.21, gamma_M=0.75, gamma_A=1.5, nitsche=15.0, g_domain=ex, f=f,
+                    exact=ex, start_t=0.0, end_t=0.1, cfl=0.3 / 9.0, cfl_pow=2.0)
+    P = wave_params()
+    return dict(P, g_domain=P["g"], g=None)
+
+
+def run_composite(simulation, max_steps=None, n=None, model=None, cfl_scale=1.0):
+    """WaveProblem<2>::run for "heat-composite" / "wave-composite"
+    (problem.h:128-214 heat-rk, :346-433 wave-rk on a BlockVector): rows
+    [(counter, t, L2, L1, Linf)] alternating inside / outside; (rows, model,
+    [operators inside, operators outside]).  At the presets' CFL the outside
+    field is outside RK4's stability region (the box corners' Nitsche mode,
+    tests/test_cut_wave2d_host.py): cfl_scale < 1 gives the stable runs."""
+    P = composite_params(simulation)
+    P["cfl"] *= cfl_scale
+    m = model or CutWave2D(P["p"], P["n"] if n is None else n, P["left"], P["right"])
+    ops = [m.matrices(P["gamma_M"], P["gamma_A"], P["nitsche"], location=loc, interface_data=False,
+                      domain_data=True, coupled=True) for loc in (INSIDE, OUTSIDE)]
+    lu = [spla.splu(o["M"].tocsc()) for o in ops]
+    N = m.N * m.N
+
+    def data(o, t):
+        r = np.zeros(N)
+        q, s = o["q"], o["s"]
+        if P["f"] is not None and q.size:
+            r += o["Ff"] @ P["f"](q[:, 0], q[:, 1], t)
+        if s.size:
+            r += o["Fg"] @ P["g_domain"](s[:, 0], s[:, 1], t)
+        return r
+
+    def fields(t, u0, u1):
+        r0 = -(ops[0]["A"] @ u0) + ops[0]["X"] @ u1 + data(ops[0], t)
+        r1 = -(ops[1]["A"] @ u1) + ops[1]["X"] @ u0 + data(ops[1], t)
+        return lu[0].solve(r0), lu[1].solve(r1)
+
+    dt = P["cfl"] * m.h ** P["cfl_pow"]
+    time = DiscreteTime(P["start_t"], P["end_t"], dt)
+    u = m.interpolate(P["exact"], P["start_t"])
+    rows = []
+
+    def post(t, u0, u1, counter):
+        rows.append((counter, t) + m.errors(ops[0], u0, P["exact"], t))
+        rows.append((counter, t) + m.errors(ops[1], u1, P["exact"], t))
+
+    post(0.0, u, u, 0)
+    if simulation == "wave-composite":
+        y = np.concatenate([u, u, np.zeros(N), np.zeros(N)])
+
+        def f(t, y):
+            a0, a1 = fields(t, y[:N], y[N:2 * N])
+            return np.concatenate([y[2 * N:3 * N], y[3 * N:], a0, a1])
+    else:
+        y = np.concatenate([u, u])
+
+        def f(t, y):
+            return np.concatenate(fields(t, y[:N], y[N:]))
+    k = 0
+    while not time.is_at_end() and (max_steps is None or k < max_steps):
+        t0, h = time.t, time.next_step_size()
+        y = rk4_step(f, t0, h, y)
+        k += 1
+        post(t0 + h, y[:N], y[N:2 * N], k)
         time.advance()
     return rows, m, ops

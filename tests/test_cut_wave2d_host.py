@@ -35,13 +35,16 @@ from test_cut_wave_host import _arr, _lib  # noqa: E402
 REF = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_outputs.json")))["wave_app"]["cases"]
 
 
-def host_system2d(prm):
-    """the device operator's host arrays (scipy CSR) for a 2D preset"""
+def host_system2d(prm, location=-1, flags=1, n=None):
+    """the device operator's host arrays (scipy CSR) for a 2D preset (the
+    field of `location`, Nitsche data / coupling `flags`, n cells per
+    direction if given)"""
     import gdm_amd.cut_wave as CW
 
     L = _lib()
     L.gdmh_cut_wave_splits.argtypes = [ctypes.c_void_p]
-    p, n, left, right = prm["p"], prm["n"], prm["left"], prm["right"]
+    p, left, right = prm["p"], prm["left"], prm["right"]
+    n = prm["n"] if n is None else n
     h = (right - left) / n
     gl = CW.gauss_lobatto(p + 1)
     x = (left + np.arange(n) * h)[:, None] + gl[None, :] * h
@@ -50,16 +53,16 @@ def host_system2d(prm):
     ls = np.ascontiguousarray(np.hypot(X, Y).reshape(-1) - 1.0)
     S = ctypes.c_void_p()
     err = ctypes.create_string_buffer(256)
-    assert L.gdmh_cut_wave_create(2, p, n, left, right, p, ls.ctypes.data, -1, 1, prm["gamma_M"], prm["gamma_A"],
+    assert L.gdmh_cut_wave_create(2, p, n, left, right, p, ls.ctypes.data, location, flags, prm["gamma_M"], prm["gamma_A"],
                                   prm["nitsche"], ctypes.byref(S), err, 256) == 0, err.value
     try:
         nd, nq, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         cells = (ctypes.c_int64 * 3)()
         L.gdmh_cut_wave_info(S, ctypes.byref(nd), ctypes.byref(nq), ctypes.byref(ns), cells)
         N, NQ, NS = nd.value, nq.value, ns.value
-        shape = {0: (N, N), 1: (N, NQ), 2: (N, NS), 3: (NQ, N), 4: (N, N), 5: (N, N)}
+        shape = {0: (N, N), 1: (N, NQ), 2: (N, NS), 3: (NQ, N), 4: (N, N), 5: (N, N), 6: (N, N)}
         out = dict(splits=L.gdmh_cut_wave_splits(S), cells=tuple(cells))
-        for w, name in enumerate(("C", "Ff", "Fg", "E", "M", "K")):
+        for w, name in enumerate(("C", "Ff", "Fg", "E", "M", "K", "X")):
             q = [ctypes.c_void_p() for _ in range(3)]
             L.gdmh_cut_wave_csr(S, w, *[ctypes.byref(v) for v in q])
             rows, cols = shape[w]
@@ -153,3 +156,64 @@ def test_device_formulation_step85():
     e = H["E"] @ u - prm["exact"](q[:, 0], q[:, 1], 0.0)
     got = (np.sqrt(np.sum(e * e * H["qw"])), np.sum(np.abs(e) * H["qw"]), np.max(np.abs(e)))
     np.testing.assert_allclose(got, REF["step85_0"]["steps"][0][2:], rtol=0, atol=2e-12)
+
+
+@pytest.fixture(scope="module")
+def composite_case():
+    """the two fields of the 2D composite presets at n = 20 (the oracle's
+    cell loops in seconds): inside and outside, domain data + coupling"""
+    prm = W.composite_params("wave-composite")
+    m = W.CutWave2D(prm["p"], 20, prm["left"], prm["right"])
+    ops = [m.matrices(prm["gamma_M"], prm["gamma_A"], prm["nitsche"], location=loc, interface_data=False,
+                      domain_data=True, coupled=True) for loc in (W.INSIDE, W.OUTSIDE)]
+    return prm, m, ops, [host_system2d(prm, loc, 2 | 4, n=20) for loc in (-1, 1)]
+
+
+def test_composite_fields_match_oracle(composite_case):
+    """both fields of heat-composite / wave-composite at dim 2 (parity
+    unpinned: the reference holds no 2D composite output): the region
+    quadrature, the domain-face data points, M, Ff, Fg, E, the own operator
+    (Z S + C) and the partner coupling X against oracle/cut_wave2d.py"""
+    prm, m, ops, H = composite_case
+    rng = np.random.default_rng(7)
+    for o, h in zip(ops, H):
+        np.testing.assert_allclose(h["qx"], o["q"][:, :2], rtol=0, atol=1e-13)
+        np.testing.assert_allclose(h["qw"], o["q"][:, 2], rtol=1e-12, atol=1e-12 * o["q"][:, 2].max())
+        np.testing.assert_allclose(h["sx"], o["s"][:, :2], rtol=0, atol=1e-13)
+        np.testing.assert_allclose(h["sn"], o["s"][:, 2:], rtol=0, atol=1e-13)
+        for name in ("M", "Ff", "Fg", "E", "X"):
+            assert h[name].shape == o[name].shape, name
+            if 0 in o[name].shape:
+                continue
+            D = (h[name] - o[name]).toarray()
+            assert abs(D).max() <= 1e-12 * max(abs(o[name]).max(), 1.0), name
+        for _ in range(2):
+            u = rng.uniform(-1, 1, m.N * m.N)
+            ref = -(o["A"] @ u)
+            assert np.abs(h["apply"](u) - ref).max() <= 1e-12 * np.abs(ref).max()
+    # the inside field has no data points (the box faces lie outside the circle), the outside field all of them
+    assert len(H[0]["sx"]) == 0 and len(H[1]["sx"]) == 4 * 20 * (prm["p"] + 1)
+    # the coupling is the transpose pair of one symmetric interface form
+    assert abs(H[0]["X"] - H[1]["X"].T).max() <= 1e-13 * abs(H[0]["X"]).max()
+
+
+def test_composite_restatement_stability():
+    """the 2D composite presets at their own CFL (wave-app.cc:152-221,
+    :286-347) are outside RK4's stability region in this restatement: the
+    outside field's corner DoFs carry the box faces' Nitsche penalty, dt
+    sqrt(lambda_max(M^-1 A)) = 3.45 > 2 sqrt(2) for wave-composite; the inside
+    field (2.14) and the inside-only wave preset (2.70) are inside it.  The
+    device runs are compared with the oracle over the first steps at the
+    presets' CFL and over whole runs at a reduced one
+    (tests/test_gpu_cut_wave2d.py)."""
+    prm = W.composite_params("wave-composite")
+    m = W.CutWave2D(prm["p"], 20, prm["left"], prm["right"])
+    dt = prm["cfl"] * m.h
+    lam = []
+    for loc in (W.INSIDE, W.OUTSIDE):
+        o = m.matrices(prm["gamma_M"], prm["gamma_A"], prm["nitsche"], location=loc, interface_data=False,
+                       domain_data=True, coupled=True)
+        lu = spla.splu(o["M"].tocsc())
+        op = spla.LinearOperator(o["A"].shape, matvec=lambda v, lu=lu, A=o["A"]: lu.solve(A @ v))
+        lam.append(abs(spla.eigs(op, k=1, which="LM", return_eigenvectors=False, maxiter=5000)[0]))
+    assert dt * np.sqrt(lam[0]) < 2 * np.sqrt(2) < dt * np.sqrt(lam[1])

@@ -73,3 +73,33 @@ def test_compute_rhs_and_mass_vs_oracle():
     Mu = cw.new_vector()
     cw.mass_apply(torch.from_numpy(xr).cuda(), Mu)
     assert np.abs(Mu.cpu().numpy() - ops["M"] @ xr).max() <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("simulation,cfl_scale,steps", [("wave-composite", 1.0, 8), ("heat-composite", 1.0, 8),
+                                                        ("wave-composite", 0.6, None), ("heat-composite", 0.5, 200)])
+def test_composite_on_device(simulation, cfl_scale, steps):
+    """the 2D composite presets (wave-app.cc:152-221, :286-347) on the device:
+    two handles (inside / outside, domain Dirichlet data on the box faces,
+    interface coupling through gdm_cut_wave_couple) against
+    oracle/cut_wave2d.run_composite, every (L2, L1, Linf) of both fields to
+    rtol 1e-7.  Parity unpinned: the reference holds no 2D composite output.
+    At the presets' own CFL the restatement is outside RK4's stability region
+    (tests/test_cut_wave2d_host.py), so those runs are compared over their
+    first 8 steps (round-off grows ~3x per step); the whole wave-composite run
+    and 200 heat-composite steps at a reduced CFL."""
+    from gdm_amd.cut_wave import CutWaveCompositeProblem, preset
+
+    P = preset(simulation, dim=2)
+    P["cfl"] *= cfl_scale
+    prob = CutWaveCompositeProblem(P)
+    m = W.CutWave2D()
+    assert prob.f[0].cells == dict(inside=int((m.loc == W.INSIDE).sum()), intersected=int((m.loc == W.INTERSECTED).sum()),
+                                   outside=int((m.loc == W.OUTSIDE).sum()))
+    rows = prob.run(max_steps=steps)
+    ref, _, _ = W.run_composite(simulation, max_steps=steps, model=m, cfl_scale=cfl_scale)
+    assert len(rows) == len(ref)
+    for got, exp in zip(rows, ref):
+        assert got[0] == exp[0] and abs(got[1] - exp[1]) <= 1e-12
+        np.testing.assert_allclose(got[2:], exp[2:], rtol=1e-7, atol=0)
+    if cfl_scale < 1.0:  # stable: the errors stay at the discretisation level
+        assert max(r[2] for r in rows) < 5e-3

@@ -284,3 +284,25 @@ def test_cut_wave_driver_reproduces_reference_output(case):
             for a, b, r in zip(g, exp[2:], rtol):
                 # printed with 9 significant digits on both sides: one more half unit of the last digit
                 assert abs(a - b) <= r * abs(b) + 5e-9 * abs(b), (got, exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("simulation", ["wave-composite", "heat-composite"])
+def test_cut_wave_driver_2d_composite(simulation):
+    """cut_wave_app 2 {wave,heat}-composite (wave-app.cc:152-221, :286-347 at
+    dim 2): the inside / outside rows of the first 8 steps against
+    oracle/cut_wave2d.run_composite (parity unpinned: no reference output; the
+    presets' CFL is outside RK4's stability region for the outside field, so
+    later steps grow, tests/test_cut_wave2d_host.py)"""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cut_wave2d as W
+
+    out = subprocess.run([CUT_WAVE_APP, "2", simulation], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    rows = [l.split() for l in out.stdout.splitlines() if l.strip()]
+    ref, _, _ = W.run_composite(simulation, max_steps=8)
+    assert len(rows) > len(ref)
+    for got, exp in zip(rows, ref):
+        assert int(got[0]) == exp[0] and abs(float(got[1]) - exp[1]) <= 5.000001e-6
+        g = np.array([float(v) for v in got[2:]])
+        np.testing.assert_allclose(g, exp[2:], rtol=2e-8, atol=0)
