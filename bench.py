@@ -348,9 +348,8 @@ def c3_rank_slab(steps=10, n_ranks=8, rank=3):
     whole = timed(lambda: apply_overlapped(op, None, u, v, bc if op.n_bc_points else None))
     interior = timed(lambda: op.apply_planes(u, v, lo, hi))
 
-    def edges():
-        op.apply_planes(u, v, pb, lo)
-        op.apply_planes(u, v, hi, pe)
+    def edges():  # both edge ranges in one launch, as apply_overlapped runs them
+        op.apply_planes2(u, v, pb, lo, hi, pe)
 
     edge = timed(edges)
     rounds = _capi.mesh_spike_rounds(op.mesh)
