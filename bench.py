@@ -202,6 +202,9 @@ def cpu_baseline(p, n_cells, threads, threads_source="--cpu-threads"):
 
 
 FP64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak (MI355X_MICROARCH.md chip table; FMA = 2 flop)
+# minimum FP64 FMA per DoF of the factored p = 5 advection stencil: x sweep 11 (mass) + 10
+# (derivative, zero centre tap), y sweep 11 + 21, z sweep 21, plus the x scale and the dint / z-mass folds
+ADV5_MIN_FMA = 77
 
 
 def c4_wave_stage(steps=10):
@@ -572,8 +575,8 @@ def main():
             if bc is not None:
                 op.add_boundary_data(bc, dst)
         else:
-            # compute_rhs in one call: interior-z stencil on the stream, z-wall launch + inflow face step 1 on
-            # the operator's side stream (fork / join), face step 2
+            # compute_rhs in one call: one stencil launch over all planes with the inflow faces' step 1 as its
+            # tail work, then face step 2 fused with the ordered adds
             op.apply(src, dst, bc)
         if ev is not None:
             ev[1].record(stream)
@@ -672,8 +675,8 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "compute_rhs = stencil8_kernel<p=%d> interior-z + z-wall launches (fused Kronecker stencil) "
-                      "+ inflow face kernels; HIP events around the whole call" % p,
+            "kernel": "compute_rhs = stencil8_kernel<p=%d> (fused Kronecker stencil, all planes, inflow face step 1 "
+                      "as tail work) + face step 2 with the ordered adds; HIP events around the whole call" % p,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -681,6 +684,11 @@ def main():
             "traffic": traffic,
             "kernel_ms": kern_ms,
             "algorithmic_bytes_per_launch": BYTES_PER_DOF * lay["n_owned"],
+            # the other bound of this kernel: FP64 VALU at the factored stencil's minimum FMA count
+            "fp64_valu": None if args.kind != "advection" or p != 5 else {
+                "fma_per_dof": ADV5_MIN_FMA, "achieved": 2.0 * ADV5_MIN_FMA * lay["n_owned"] / (kern_ms * 1e-3) / 1e12,
+                "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": 2.0 * ADV5_MIN_FMA * lay["n_owned"] / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFS},
             "mass_solve": mass,
         },
         "rk4_stage_ms": stage_ms,
