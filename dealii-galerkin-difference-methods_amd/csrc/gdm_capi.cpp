@@ -1119,6 +1119,13 @@ void build_spike(gdm_op *op) {
 #ifndef GDM_MASS_X_STRIDED
 #define GDM_MASS_X_STRIDED 0
 #endif
+// strided lines no longer than one v3 chunk (a slab's z lines at C4 on 8 ranks:
+// 32 planes) run the two-sweep kernel: the single-sweep one spends such a line
+// in its table-row path (every row of a 32-line is a boundary row); C4 rank
+// SPIKE solve 0.146 -> 0.142 ms (profiles/r5_experiments/README.md)
+#ifndef GDM_MASS_SHORT_V2
+#define GDM_MASS_SHORT_V2 1
+#endif
 // rk (single rank): the RK stage update of gdm_mass_solve_rk fused into the
 // last pass when that is the unsegmented v3 x pass; returns whether it was
 // (else x_owned holds M^-1 rhs and the caller updates)
@@ -1168,6 +1175,9 @@ bool mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
 #endif
   auto use_v3 = [&](const Pass &q, const double *src, const double *dst) {
     const LineTables &t = tab[q.ax];
+#if GDM_MASS_SHORT_V2
+    if (q.dir_kind == 1 && q.len <= gdmk_mass3_chunk(op->p)) return false;
+#endif
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
     // the v3 strided kernel addresses a wave's 64 lines through one buffer
     // resource (num_records 0x7fffffff) with 32-bit position offsets: the
