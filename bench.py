@@ -46,6 +46,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--rank-timeout", type=float, default=1800.0,
+                    help="--gpus N without a launcher: seconds before hung rank processes are terminated")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=511, help="cells per direction per GPU slab (vertices = n + 1)")
     ap.add_argument("--p", type=int, default=5)
@@ -479,34 +481,67 @@ def _free_port():
         return so.getsockname()[1]
 
 
-def spawn_ranks(n, cmd, env=None, poll_s=0.2):
+def spawn_ranks(n, cmd, env=None, poll_s=0.2, timeout_s=None):
     """Run `cmd` as n rank processes of one job on this node (one per GPU):
     each child gets RANK = LOCAL_RANK = r, WORLD_SIZE = n, MASTER_ADDR =
     127.0.0.1 and a free MASTER_PORT, and inherits stdout / stderr (rank 0
     prints the JSON line).  Returns 0 when every child exits 0, else the first
     non-zero exit code seen (a child killed by signal s gives 128 + s); the
     other children are then terminated by PID, so that none is left waiting in
-    a collective.  The caller must not have touched the GPU."""
+    a collective.  timeout_s (None: no limit): past it every child still
+    running is terminated and 124 returned (a rank hung in a collective never
+    exits by itself).  An exception in the parent -- SIGINT, or SIGTERM, which
+    is turned into one -- terminates the children too (try / finally), then
+    kills any that ignore SIGTERM for 10 s.  The caller must not have touched
+    the GPU.  (MASTER_PORT is probed free here and bound by rank 0's store a
+    moment later; another process taking it in between fails the job's
+    rendezvous loudly, it does not hang.)"""
+    import signal
+
     base = dict(os.environ if env is None else env)
     base.update({"WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port())})
     procs = []
-    for r in range(n):
-        e = dict(base)
-        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(n)})
-        procs.append(subprocess.Popen(cmd, env=e))
+
+    def _term(signum, frame):
+        raise KeyboardInterrupt("signal %d" % signum)
+
+    old_term = signal.signal(signal.SIGTERM, _term)
     rc = 0
-    live = list(procs)
-    while live:
-        for pr in list(live):
-            c = pr.poll()
-            if c is None:
-                continue
-            live.remove(pr)
-            if c != 0 and rc == 0:
-                rc = c if c > 0 else 128 - c
-                for other in live:
-                    other.terminate()
-        time.sleep(poll_s)
+    try:
+        for r in range(n):
+            e = dict(base)
+            e.update({"RANK": str(r), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(n)})
+            procs.append(subprocess.Popen(cmd, env=e))
+        t_end = None if timeout_s is None else time.monotonic() + timeout_s
+        live = list(procs)
+        while live:
+            for pr in list(live):
+                c = pr.poll()
+                if c is None:
+                    continue
+                live.remove(pr)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    for other in live:
+                        other.terminate()
+            if live and t_end is not None and time.monotonic() > t_end:
+                for pr in live:
+                    pr.terminate()
+                if rc == 0:
+                    rc = 124
+                t_end = None
+            time.sleep(poll_s)
+    finally:
+        signal.signal(signal.SIGTERM, old_term)
+        stragglers = [pr for pr in procs if pr.poll() is None]
+        for pr in stragglers:
+            pr.terminate()
+        for pr in stragglers:
+            try:
+                pr.wait(10)
+            except subprocess.TimeoutExpired:
+                pr.kill()
+                pr.wait()
     return rc
 
 
@@ -521,7 +556,7 @@ def main():
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         # no launcher: start the ranks here (before anything initialises the GPU)
-        sys.exit(spawn_ranks(args.gpus, rank_command(sys.argv[1:])))
+        sys.exit(spawn_ranks(args.gpus, rank_command(sys.argv[1:]), timeout_s=args.rank_timeout))
     if world_env is not None and int(world_env) != args.gpus:
         print("bench.py: WORLD_SIZE=%s but --gpus %d" % (world_env, args.gpus), file=sys.stderr)
         sys.exit(2)

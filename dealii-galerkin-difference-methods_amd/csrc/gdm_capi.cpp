@@ -159,9 +159,8 @@ struct gdm_op {
   std::vector<Face> faces;
   double *face_tmp = nullptr;
   // the stencil's tail work (face step 1, gdmk_launch_stencil8): device claim
-  // counter and the next launch's first claim
+  // counter, 0 between launches (each launch resets it with its last claim)
   unsigned long long *tail_counter = nullptr;
-  unsigned long long tail_base = 0;
   double *mass_tmp = nullptr;  // ping-pong vector of the segmented mass passes (small meshes)
   int64_t mass_tmp_size = 0;
   int64_t face_tmp_size = 0;
@@ -761,13 +760,10 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
   a.zchunk = (int)std::max<int64_t>(std::min(len, 8), (len + chunks - 1) / chunks);
   a.nchunk0 = (ze - zb + a.zchunk - 1) / a.zchunk;
   const bool with_tail = n_tail > 0 && tail && op->tail_counter;
-  unsigned long long claims = 0;
+  bool ran = false;
   const hipError_t e = gdmk_launch_stencil8(op->p, bk, a, with_tail ? tail : nullptr, with_tail ? n_tail : 0,
-                                            op->tail_counter, op->tail_base, &claims, op->stream);
-  if (e == hipSuccess) {
-    op->tail_base += claims;
-    if (tail_done) *tail_done = claims > 0;
-  }
+                                            op->tail_counter, &ran, op->stream);
+  if (e == hipSuccess && tail_done) *tail_done = ran;
   return e;
 }
 
@@ -1116,16 +1112,6 @@ void build_spike(gdm_op *op) {
 
 // the line solves of M^-1 along every kernel axis; `part` replaces the
 // partitioned axis' tables by the slab's diagonal block (multi-rank)
-#ifndef GDM_MASS_X_STRIDED
-#define GDM_MASS_X_STRIDED 0
-#endif
-// strided lines no longer than one v3 chunk (a slab's z lines at C4 on 8 ranks:
-// 32 planes) run the two-sweep kernel: the single-sweep one spends such a line
-// in its table-row path (every row of a 32-line is a boundary row); C4 rank
-// SPIKE solve 0.146 -> 0.142 ms (profiles/r5_experiments/README.md)
-#ifndef GDM_MASS_SHORT_V2
-#define GDM_MASS_SHORT_V2 1
-#endif
 // rk (single rank): the RK stage update of gdm_mass_solve_rk fused into the
 // last pass when that is the unsegmented v3 x pass; returns whether it was
 // (else x_owned holds M^-1 rhs and the caller updates)
@@ -1166,18 +1152,14 @@ bool mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
   const bool part_z = part && op->part_axis == 2, part_y = part && op->part_axis == 1;
   if (Z > 1 || part_z) passes.push_back({2, 1, Z, X * Y, X * Y, X * Y, 0, "mass z"});  // base = l, step X*Y
   if (Y > 1 || part_y) passes.push_back({1, 1, Y, X, X * Z, X, X * Y, "mass y"});      // base = z*X*Y + x, step X
-#if GDM_MASS_X_STRIDED
-  // x lines through the strided (lane = line) kernel: line l at l X, step 1 -- every load / store instruction
-  // touches 64 rows; no LDS staging, so four waves per CU
-  if (X > 1) passes.push_back({0, 1, X, 1, Y * Z, 1, X, "mass x"});
-#else
   if (X > 1) passes.push_back({0, 0, X, 1, Y * Z, 1, 0, "mass x"});                   // contiguous rows of length X
-#endif
   auto use_v3 = [&](const Pass &q, const double *src, const double *dst) {
     const LineTables &t = tab[q.ax];
-#if GDM_MASS_SHORT_V2
+    // strided lines no longer than one v3 chunk (a slab's z lines at C4 on 8
+    // ranks: 32 planes) run the two-sweep kernel: the single-sweep one spends
+    // such a line in its table-row path (every row of a 32-line is a boundary
+    // row); C4 rank SPIKE solve 0.146 -> 0.142 ms (profiles/r5_experiments)
     if (q.dir_kind == 1 && q.len <= gdmk_mass3_chunk(op->p)) return false;
-#endif
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
     // the v3 strided kernel addresses a wave's 64 lines through one buffer
     // resource (num_records 0x7fffffff) with 32-bit position offsets: the
@@ -1518,6 +1500,15 @@ int gdm_apply_planes2(gdm_op *op, const double *src_local, double *dst_owned, in
   if (op->layout.n_owned > 0 && (!src_local || !dst_owned)) return fail(GDM_ERR_ARG, "NULL vector");
   if (op->part_axis != 2) return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_planes2: plane ranges need a 3D mesh");
   if (op->mesh.periodic) return fail(GDM_ERR_UNSUPPORTED, "gdm_apply_planes2: periodic constraints");
+  // clip both ranges to the owned planes first (a first range in
+  // the ghost planes must not drop the second), then test overlap and emptiness
+  {
+    const int ob = op->layout.owned_plane_begin, oe = op->layout.owned_plane_end;
+    b0 = std::max(b0, ob);
+    e0 = std::min(e0, oe);
+    b1 = std::max(b1, ob);
+    e1 = std::min(e1, oe);
+  }
   if (e0 > b0 && e1 > b1 && b1 < e0 && b0 < e1) return fail(GDM_ERR_ARG, "gdm_apply_planes2: overlapping ranges");
   GDM_GUARD_BEGIN
   hip_check(hipSetDevice(op->device), "hipSetDevice");

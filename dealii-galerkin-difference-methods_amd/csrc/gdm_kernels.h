@@ -121,11 +121,11 @@ hipError_t gdmk_launch_stencil(int p, int bk, const gdmk::StencilArgs &a, hipStr
 // v8: output planes [cz0[r], cz1[r]) in chunks of zchunk, z-wall planes included.
 // Tail work: the workgroups that finish their chunk run step 1 of the inflow
 // faces tail_faces[0, n_tail) (cell form, own T each) in row blocks claimed from
-// the device counter; this launch's claims are [base, base + *claims) (the
-// caller's next base); n_tail = 0: no tail work, *claims = 0.
+// the device counter (0 between launches: the launch's last claim resets it);
+// *tail_ran: the tail was launched.  n_tail = 0: no tail work.  Launches that
+// share a counter must be stream-ordered.
 hipError_t gdmk_launch_stencil8(int p, int bk, const gdmk::StencilArgs &a, const gdmk::FaceArgs *tail_faces, int n_tail,
-                                unsigned long long *counter, unsigned long long base, unsigned long long *claims,
-                                hipStream_t st);
+                                unsigned long long *counter, bool *tail_ran, hipStream_t st);
 int gdmk_stencil_tile_rows(int p);
 void gdmk_stencil8_geom(int p, int *tile_rows, int *wgs_per_cu);
 hipError_t gdmk_launch_chol_lines(int p, double *v, int len, int64_t stride, int64_t n_lines, int64_t A, int64_t B,

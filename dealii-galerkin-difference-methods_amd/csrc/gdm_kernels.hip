@@ -1376,14 +1376,6 @@ __device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[s][j] = 0.0;
   GDM_LDS_BARRIER();  // tables in LDS, counters zeroed
-#ifdef GDM_X_STAGGER
-  if (GDM_X_STAGGER_SEL) {
-    for (int q = 0; q < GDM_X_STAGGER; ++q) __builtin_amdgcn_s_sleep(8);
-  }
-#endif
-#ifdef GDM_X_PRIOHALF
-  if (t.cw >= NC / 2) __builtin_amdgcn_s_setprio(1);
-#endif
   // Input plane zz scatters with its z column: a wall column for zz < W or
   // zz >= Nz - W (LDS table), else the interior one.  Blocks of W planes that
   // hold a wall column run the table path for all their planes, the others
@@ -1424,15 +1416,17 @@ __device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) 
 // counter.  One workgroup per CU and one round: the wall tiles finish last,
 // and this fills their tail.  A separate side-stream launch of the same work
 // starved the stencil instead: its small workgroups took the CUs that the
-// stencil's whole-CU workgroups were waiting for.  The counter only grows:
-// this launch owns [base, base + items + gridDim), every workgroup ending with
-// one claim past the items.
+// stencil's whole-CU workgroups were waiting for.  Each launch is
+// self-contained: the counter is 0 when it starts, every workgroup ends with
+// one claim past the items, and the workgroup that makes the launch's last
+// claim (items + workgroups - 1) sets it back to 0 -- all other claims have
+// been made by then -- so stream-ordered launches and graph replays need no
+// host-side state.
 struct StencilTail {
   Step1Set<BcArr> s1;
   int nfaces, items;
   int first[BcStage::kMaxFaces + 1];  // item range of face f: [first[f], first[f + 1])
   unsigned long long *counter;
-  unsigned long long base;
 };
 
 template <int P>
@@ -1440,7 +1434,10 @@ __device__ __forceinline__ void stencil_tail(const StencilTail &tl, lu32 *slot) 
   __syncthreads();  // every role is done with the LDS
   while (true) {
     if (threadIdx.x == 0) {
-      const unsigned long long v = atomicAdd(tl.counter, 1ull) - tl.base;
+      const unsigned long long v = atomicAdd(tl.counter, 1ull);
+      const unsigned long long last =
+          (unsigned long long)tl.items + (unsigned long long)gridDim.x * gridDim.y * gridDim.z - 1ull;
+      if (v == last) atomicExch(tl.counter, 0ull);  // the launch's last claim: reset for the next launch
       *slot = (unsigned)(v < (unsigned long long)tl.items ? v : (unsigned long long)tl.items);
     }
     __syncthreads();
@@ -1815,13 +1812,13 @@ static hipError_t launch7_p(int bk, const StencilArgs &a, hipStream_t st) {
 struct TailReq {
   const FaceArgs *faces;
   int n;
-  unsigned long long *counter, base, *claims;
+  unsigned long long *counter;
+  bool *ran;
 };
 
 // the tail work of a launch: step 1 of the faces fa[0, nf) (cell form, each its
 // own T); items = 0 when nf = 0 or a face cannot run in the tail
-static StencilTail make_tail(const FaceArgs *fa, int nf, int p, unsigned long long *counter,
-                             unsigned long long base, size_t lds_avail) {
+static StencilTail make_tail(const FaceArgs *fa, int nf, int p, unsigned long long *counter, size_t lds_avail) {
   StencilTail tl{};
   if (nf <= 0 || nf > BcStage::kMaxFaces || !counter) return tl;
   // rows per item: as many as the launch's LDS holds (the rows form keeps
@@ -1846,7 +1843,6 @@ static StencilTail make_tail(const FaceArgs *fa, int nf, int p, unsigned long lo
   tl.nfaces = nf;
   tl.items = items;
   tl.counter = counter;
-  tl.base = base;
   return tl;
 }
 
@@ -1866,12 +1862,10 @@ static hipError_t launch8_t(const StencilArgs &a, const TailReq &tr, hipStream_t
     if (a.cz1[r] > a.cz0[r]) nz += (a.cz1[r] - a.cz0[r] + a.zchunk - 1) / a.zchunk;
   dim3 grid((a.Nx + G::TX - 1) / G::TX, (a.out_y1 - a.out_y0 + G::TY - 1) / G::TY, nz);
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return hipSuccess;
-  const StencilTail tail = make_tail(tr.faces, tr.n, P, tr.counter, tr.base, lds);
+  const StencilTail tail = make_tail(tr.faces, tr.n, P, tr.counter, lds);
   hipLaunchKernelGGL((stencil8_kernel<P, R, NC, NP, BK, CH, PF>), grid, dim3(G::NT), lds, st, a, tail);
   const hipError_t e = hipGetLastError();
-  // counter claims of this launch: every item once, and one past the end per workgroup
-  if (e == hipSuccess && tail.items > 0)
-    *tr.claims = (unsigned long long)tail.items + (unsigned long long)grid.x * grid.y * grid.z;
+  if (e == hipSuccess && tail.items > 0) *tr.ran = true;
   return e;
 }
 
@@ -1896,11 +1890,11 @@ static hipError_t launch8_p(int bk, const StencilArgs &a, const TailReq &tail, h
 }  // namespace gdmk
 
 extern "C" hipError_t gdmk_launch_stencil8(int p, int bk, const gdmk::StencilArgs &a, const gdmk::FaceArgs *tail_faces,
-                                           int n_tail, unsigned long long *counter, unsigned long long base,
-                                           unsigned long long *claims, hipStream_t st) {
+                                           int n_tail, unsigned long long *counter, bool *tail_ran,
+                                           hipStream_t st) {
   using namespace gdmk;
-  *claims = 0;
-  const TailReq tail{tail_faces, n_tail, counter, base, claims};
+  *tail_ran = false;
+  const TailReq tail{tail_faces, n_tail, counter, tail_ran};
   hipError_t e = hipErrorInvalidValue;
   switch (p) {
 #if !defined(GDM_ONLY_P) || GDM_ONLY_P == 1

@@ -289,13 +289,9 @@ struct Geo3 {
   // strided: loads in flight per lane.  One chunk ahead: with the 2C-double
   // ring this runs one wave per SIMD, so the FIFO alone must cover the HBM
   // latency (Q * 512 B per wave; a 16-deep FIFO measured as latency-bound)
-#ifdef GDM_MASS_Q5
-  static constexpr int Q = P == 5 ? GDM_MASS_Q5 : (P < 5 ? C : C / 2);
-#else
   // with the stores streamed between the loads (Ring3::fwd ST), load j waits
   // for vmcnt <= ~2 Q: Q = C / 2 <= 31 keeps that within the 6-bit counter
   static constexpr int Q = P <= 5 ? C / 2 : C / 4;  // p = 7: C / 2 spills to scratch
-#endif
   static constexpr int QL = 4;                // rows: LDS pair reads ahead
   static constexpr int UPR = (C + 2) / 2;     // rows: 16-B units per LDS row (pitch C + 2 doubles)
   static constexpr int TILE = 64 * UPR;       // rows: units per tile (= 64 x DMA instructions)
@@ -303,13 +299,6 @@ struct Geo3 {
   static_assert(C % Q == 0 && C % 4 == 0, "chunk geometry");
 };
 
-#ifdef GDM_MASS_WPE
-#define GDM_MASS_STRIDED_ATTR __attribute__((amdgpu_waves_per_eu(GDM_MASS_WPE)))
-#else
-#define GDM_MASS_STRIDED_ATTR
-#endif
-
-// line-end chunks: 2 = per-group table / interior-row decision, 1 = tables for the whole chunk
 // cache policy of the v3 kernels' global accesses (buffer aux bits on gfx950:
 // 2 = nt): the line data stream through once per pass, so loads and stores are
 // non-temporal.  A/B on the MI355X (profiles/r3v, mass solve): C3 1.515 ->
@@ -321,9 +310,9 @@ struct Geo3 {
 #ifndef GDM_MASS_ST_CPOL
 #define GDM_MASS_ST_CPOL 2
 #endif
-#ifndef GDM_MASS_EDGE_MODE
+// line-end chunks take their table rows for the whole chunk (a per-group
+// table / interior-row decision measured slower: SGPR spills, round 2)
 #define GDM_MASS_EDGE_MODE 1
-#endif
 
 // compiler-only fence: the scheduler may not move instructions across it
 #define GDM_FENCE()                    \
@@ -508,7 +497,7 @@ struct Ring3 {
 // mass_solve_passes in gdm_capi.cpp, which runs the 64-bit-addressed v2
 // kernel for larger spans).  src may equal dst.
 template <int P, bool SEG>
-__global__ void __launch_bounds__(64) GDM_MASS_STRIDED_ATTR mass3_strided_kernel(const double *src, double *dst, int len, int64_t stride,
+__global__ void __launch_bounds__(64) mass3_strided_kernel(const double *src, double *dst, int len, int64_t stride,
                                                            int64_t n_lines, int64_t A, int64_t B,
                                                            const double *__restrict__ lrow,
                                                            const double *__restrict__ urow,

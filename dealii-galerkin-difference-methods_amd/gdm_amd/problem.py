@@ -145,9 +145,16 @@ class AdvectionProblem:
         return self._bc
 
     def initialize_time_step(self, t):
-        """block(0) = g(t_n) at the boundary points (stiffness.h:181-194)"""
+        """block(0) = g(t_n) at the boundary points (stiffness.h:181-194).
+        With carry_bc=False there is no block(0) to fill: step() has the
+        engine evaluate g(t_n) (+ the stage terms) right before each stencil,
+        so this is a no-op and returns False; True when block(0)
+        was written."""
+        if not self.carry_bc:
+            return False
         if self.op.n_bc_points:
             self.op.eval_boundary(self.fn, self.prm, t, 0, self.bc)
+        return True
 
     def rhs(self, t, BC, U, kbc, ku):
         op = self.op

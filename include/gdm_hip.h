@@ -167,7 +167,10 @@ int gdm_halo_plan(const gdm_mesh_desc *mesh, gdm_halo *out);
 int gdm_op_layout(const gdm_op *op, gdm_layout *out);
 /* launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream;
  * NULL is the HIP null stream); gdm_op_use_own_stream restores the operator's
- * private non-blocking stream */
+ * private non-blocking stream.  An operator's calls must stay ordered (one
+ * stream at a time, or the caller orders the streams): they share the
+ * operator's face scratch and the stencil's tail-work counter.  Each call is
+ * self-contained otherwise, so it may be captured in a hipGraph and replayed. */
 int gdm_op_set_stream(gdm_op *op, void *hip_stream);
 int gdm_op_use_own_stream(gdm_op *op);
 /* the hipStream_t the operator launches on now (set or own): a communicator
@@ -190,7 +193,8 @@ int gdm_apply_planes(gdm_op *op, const double *src_local, double *dst_owned, int
 /* gdm_apply_planes of two plane ranges [b0, e0) and [b1, e1) in ONE launch
  * (ABI 13): the p planes next to both slab edges after the exchange, so the
  * thin edge ranges share the GPU instead of running one after the other.  The
- * same bits as two gdm_apply_planes calls.  An empty range is allowed. */
+ * same bits as two gdm_apply_planes calls.  Both ranges are clipped to the
+ * owned planes first; an empty (or wholly unowned) range is allowed. */
 int gdm_apply_planes2(gdm_op *op, const double *src_local, double *dst_owned, int b0, int e0, int b1, int e1);
 /* dst_owned += inflow boundary-data term only (the bc part of gdm_apply,
  * advection/stiffness.h:520-529 with a.n < 0); no-op for other kinds */

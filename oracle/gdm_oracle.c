@@ -529,6 +529,97 @@ int gdmo_advection_rhs(int dim, int p, const unsigned *nsub, const double *lo, c
 }
 
 /* ------------------------------------------------------------------------- */
+/* The inflow-data part of gdmo_advection_rhs alone: term (III) of            */
+/* stiffness.h:473-532 with u = 0, i.e. rhs_i -= (a.n) u+ phi_i JxW on the box */
+/* faces with a.n < 0.  Only the boundary cells are visited, in cell order,   */
+/* with the reference's point_counter over every boundary face point          */
+/* (stiffness.h:337), so stage_bc is the same reference-ordered block(0) as   */
+/* gdmo_advection_rhs reads; the face shape values are cached per category    */
+/* tuple and face.  Equals gdmo_advection_rhs(u = 0, stage_bc) term by term   */
+/* (tests/test_oracle_golden.py), at the cost of the O(n^(dim-1)) boundary    */
+/* cells: the full-size C3 inflow check of tests/test_gpu_fullsize.py.        */
+/* ------------------------------------------------------------------------- */
+int gdmo_advection_inflow(int dim, int p, const unsigned *nsub, const double *lo, const double *hi,
+                          const double *a, const double *stage_bc, double *rhs)
+{
+  tables_t T;
+  build_tables(&T, dim, p);
+  const int nd = T.nd, n1 = p + 1, nfq = n_face_q(dim, p);
+  const int ncat = (p == 1) ? 1 : p;
+  const size_t tsz = (size_t)nfq * nd;
+  /* face shape tables, key (cat0, cat1, cat2, f), computed on first use */
+  const size_t nkeys = (size_t)ncat * ncat * ncat * 6;
+  double **fs = (double **)calloc(nkeys, sizeof(double *));
+  uint64_t *dofs = (uint64_t *)malloc(sizeof(uint64_t) * nd);
+  double *cv = (double *)malloc(sizeof(double) * nd);
+  unsigned n[3] = {1, 1, 1};
+  for (int d = 0; d < dim; ++d)
+    n[d] = nsub[d];
+  uint64_t pc = 0;
+  /* rows of cells along x: a row is all boundary cells when any higher
+   * coordinate is on the boundary, else only its first and last cell */
+  for (unsigned cz = 0; cz < n[2]; ++cz)
+    for (unsigned cy = 0; cy < n[1]; ++cy) {
+      const int row_bdry = (dim >= 2 && (cy == 0 || cy == n[1] - 1)) || (dim >= 3 && (cz == 0 || cz == n[2] - 1));
+      for (unsigned cx = 0; cx < n[0]; ++cx) {
+        if (!row_bdry && cx != 0 && cx != n[0] - 1) {
+          cx = n[0] - 2; /* skip the interior of the row */
+          continue;
+        }
+        const unsigned c = cx + n[0] * (cy + n[1] * cz);
+        unsigned cidx[3], cat[3];
+        double h[3];
+        cell_setup(dim, p, nsub, c, lo, hi, cidx, cat, h);
+        int any = 0;
+        for (int i = 0; i < nd; ++i)
+          cv[i] = 0.0;
+        for (int f = 0; f < 2 * dim; ++f) {
+          const int d = f / 2, side = f % 2;
+          const int at = side ? (cidx[d] == nsub[d] - 1) : (cidx[d] == 0);
+          if (!at)
+            continue;
+          const double an = side ? a[d] : -a[d]; /* a . n */
+          if (an >= 0.0) {
+            pc += nfq; /* outflow face: u = 0 contributes nothing */
+            continue;
+          }
+          const size_t key = (((size_t)cat[0] * ncat + cat[1]) * ncat + cat[2]) * 6 + f;
+          if (!fs[key]) {
+            fs[key] = (double *)malloc(sizeof(double) * tsz);
+            for (int q = 0; q < nfq; ++q) {
+              int qq[3];
+              face_point(dim, f, q, n1, qq);
+              for (int i = 0; i < nd; ++i)
+                fs[key][(size_t)q * nd + i] = face_shape(&T, cat, i, qq, side);
+            }
+          }
+          const double *tab = fs[key];
+          for (int q = 0; q < nfq; ++q) {
+            int qq[3];
+            face_point(dim, f, q, n1, qq);
+            const double jxw = face_jxw(&T, dim, f, qq, h);
+            const double uplus = stage_bc[pc++];
+            for (int i = 0; i < nd; ++i)
+              cv[i] += an * (0.0 * 0.0 - uplus) * tab[(size_t)q * nd + i] * jxw;
+          }
+          any = 1;
+        }
+        if (!any)
+          continue;
+        gdmo_cell_dof_indices(dim, p, nsub, c, dofs);
+        for (int i = 0; i < nd; ++i)
+          rhs[dofs[i]] += cv[i];
+      }
+    }
+  for (size_t k = 0; k < nkeys; ++k)
+    free(fs[k]);
+  free(fs);
+  free(dofs);
+  free(cv);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
 /* Convective-form rhs of prototypes/advection_01_gdm.cc:164-206:             */
 /* cell_i -= (a . grad u_q) phi_i JxW  (no face terms; constraints applied by */
 /* the caller).                                                                */

@@ -49,6 +49,7 @@ def lib():
         L.gdmo_n_boundary_points.argtypes = [i, i, P, u, u]
         L.gdmo_boundary_points.argtypes = [i, i, P, P, P, u, u, P]
         L.gdmo_advection_rhs.argtypes = [i, i, P, P, P, P, P, P, P, u, u]
+        L.gdmo_advection_inflow.argtypes = [i, i, P, P, P, P, P, P]
         L.gdmo_convective_rhs.argtypes = [i, i, P, P, P, P, P, P]
         L.gdmo_wave_rhs.argtypes = [i, i, P, P, P, P, i, P, d, P, P, u, u]
         L.gdmo_matrix_csr.restype = i64
@@ -148,6 +149,17 @@ class Mesh:
         bc = None if stage_bc is None else np.ascontiguousarray(stage_bc, dtype=np.float64)
         lib().gdmo_advection_rhs(self.dim, self.p, _p(self.nsub), _p(self.lo), _p(self.hi), _p(a3), _p(u),
                                  _p(bc) if bc is not None else None, _p(out), cb, ce)
+        return out
+
+    def advection_inflow(self, a, stage_bc):
+        """The inflow-data part of advection_rhs alone (u = 0), visiting only
+        the boundary cells: gdmo_advection_inflow"""
+        a3 = _d3(a, self.dim)
+        bc = np.ascontiguousarray(stage_bc, dtype=np.float64)
+        assert bc.size == self.n_boundary_points()
+        out = np.zeros(self.n_dofs)
+        lib().gdmo_advection_inflow(self.dim, self.p, _p(self.nsub), _p(self.lo), _p(self.hi), _p(a3), _p(bc),
+                                    _p(out))
         return out
 
     def convective_rhs(self, a, u):

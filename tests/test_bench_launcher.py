@@ -46,6 +46,44 @@ def test_spawn_ranks_propagates_failure_and_stops_the_rest():
     assert time.time() - t0 < 30  # the sleeping rank was terminated, not waited for
 
 
+def test_spawn_ranks_timeout_terminates_hung_ranks():
+    """a rank hung without exiting (here: sleeping) ends the job
+    at the timeout with rc 124 and no child left behind"""
+    t0 = time.time()
+    rc = bench.spawn_ranks(2, [sys.executable, "-c", STUB], env=_env(SLEEP_RANK="1"), timeout_s=2.0)
+    assert rc == 124
+    assert time.time() - t0 < 30
+
+
+def test_spawn_ranks_parent_interrupt_terminates_children(monkeypatch):
+    """an exception in the parent's wait loop (SIGINT / SIGTERM) terminates
+    the children before it propagates"""
+    started = []
+    real_popen = subprocess.Popen
+
+    def popen(*a, **kw):
+        pr = real_popen(*a, **kw)
+        started.append(pr)
+        return pr
+
+    calls = {"n": 0}
+
+    def sleep(_):
+        calls["n"] += 1
+        if calls["n"] == 3:
+            raise KeyboardInterrupt
+
+    monkeypatch.setattr(bench.subprocess, "Popen", popen)
+    monkeypatch.setattr(bench.time, "sleep", sleep)
+    try:
+        bench.spawn_ranks(2, [sys.executable, "-c", STUB], env=_env(SLEEP_RANK="0"))
+    except KeyboardInterrupt:
+        pass
+    else:
+        raise AssertionError("KeyboardInterrupt not propagated")
+    assert len(started) == 2 and all(pr.poll() is not None for pr in started)
+
+
 def test_rank_command_reuses_the_parent_arguments():
     cmd = bench.rank_command(["--gpus", "8", "--steps", "5", "--warmup", "2"])
     assert cmd[0] == sys.executable and os.path.basename(cmd[1]) == "bench.py"

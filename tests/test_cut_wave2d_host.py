@@ -217,3 +217,20 @@ def test_composite_restatement_stability():
         op = spla.LinearOperator(o["A"].shape, matvec=lambda v, lu=lu, A=o["A"]: lu.solve(A @ v))
         lam.append(abs(spla.eigs(op, k=1, which="LM", return_eigenvectors=False, maxiter=5000)[0]))
     assert dt * np.sqrt(lam[0]) < 2 * np.sqrt(2) < dt * np.sqrt(lam[1])
+
+
+@pytest.mark.parametrize("name", ["wave-composite", "heat-composite"])
+def test_composite_preset_2d_warns_about_its_cfl(name):
+    """the 2D composite presets carry the reference's CFL, at which
+    the outside field is unstable in this restatement; preset() says so (1D
+    composite presets, pinned by the reference's goldens, do not warn)"""
+    import warnings
+
+    import gdm_amd.cut_wave as CW
+
+    with pytest.warns(RuntimeWarning, match="unstable"):
+        P = CW.preset(name, 2)
+    assert P["simulation"] == name and P["dim"] == 2
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        CW.preset(name, 1)

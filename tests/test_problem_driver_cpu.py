@@ -131,3 +131,17 @@ def test_advection_no_block0_vectors_without_carry_bc(no_torch):
         pr.bc
     pr2 = AdvectionProblem(_Op(), 2, [0.0] * 9, carry_bc=True)
     assert pr2.bc is not None and pr2._acc[0] is not None
+
+
+def test_advection_initialize_time_step_without_carry_bc(no_torch):
+    """the public initialize_time_step() stays callable on the
+    default (engine-computed boundary values) path -- a no-op there -- and
+    fills block(0) on the explicit path"""
+    op = _Op()
+    pr = AdvectionProblem(op, 2, [0.0] * 9)
+    assert pr.initialize_time_step(0.5) is False
+    assert op.calls == []
+    op2 = _Op()
+    pr2 = AdvectionProblem(op2, 2, [0.0] * 9, carry_bc=True)
+    assert pr2.initialize_time_step(0.5) is True
+    assert [c[0] for c in op2.calls] == ["eval_boundary"] and op2.calls[0][1][2] == 0.5
