@@ -130,7 +130,7 @@ struct gdm_op {
   // v8 variants: E pre-scaled by h_z (sx, cy, corrX's B part, yT3), z table e = M_z / h_z
   double *corrX8 = nullptr, *yT3_8 = nullptr, *zt8 = nullptr;
   double *yT1d = nullptr, *yT3d = nullptr, *m_yT3d = nullptr;  // v8 y corrections
-  double sx8 = 0, cy8[19] = {0};
+  double sx8 = 0, cy8[19] = {0}, cxs8[19] = {0};
   double dint = 0, m_dint = 0;  // interior z scales of D (operator, mass)
   double zd8[19] = {0}, m_zd8[19] = {0};  // dint * dhat[2p - k] (operator, mass)
   int xcd_map = 1;
@@ -476,6 +476,7 @@ void build_tables(gdm_op *op) {
     const gdm::Band Mz8 = scaled(M[2], 1.0 / h[2]);
     op->zt8 = keep(op, dev_upload(z_table(&Mz8, Bz, 1.0, beta[2] * h[0] * h[1], bhat)));
     op->sx8 = op->sx * h[2];
+    for (int k = 0; k < W; ++k) op->cxs8[k] = op->sx8 * bhat[k];
     op->dint = beta[2] * h[0] * h[1];
     for (int k = 0; k < W; ++k) op->zd8[k] = op->dint * bhat[2 * p - k];
     for (int k = 0; k < W; ++k) op->cy8[k] = op->cy[k] * h[2];
@@ -724,6 +725,7 @@ hipError_t launch_stencil(gdm_op *op, bool mass, const double *src, double *dst,
     a.dint = op->dint;
     for (int k = 0; k < 19; ++k) a.zd[k] = op->zd8[k];
     a.sx = op->sx8;
+    for (int k = 0; k < 19; ++k) a.cxs[k] = op->cxs8[k];
     for (int k = 0; k < 19; ++k) a.cy[k] = op->cy8[k];
     a.corrX = op->corrX8;
     a.yT3 = op->yT3d;
@@ -1655,7 +1657,13 @@ int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned) {
   GDM_GUARD_END
 }
 
-int gdm_mass_solve_interface(gdm_op *op, double *x_local) {
+static int mass_solve_interface_impl(gdm_op *op, double *x_local, bool ghosts);
+
+int gdm_mass_solve_interface(gdm_op *op, double *x_local) { return mass_solve_interface_impl(op, x_local, false); }
+
+int gdm_mass_solve_interface_ghosts(gdm_op *op, double *x_local) { return mass_solve_interface_impl(op, x_local, true); }
+
+static int mass_solve_interface_impl(gdm_op *op, double *x_local, bool ghosts) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   if (op->mesh.n_ranks == 1) return GDM_OK;
   if (!op->spike.built || op->spike.rounds < 0 || op->spike.next_round < 0)
@@ -1673,11 +1681,11 @@ int gdm_mass_solve_interface(gdm_op *op, double *x_local) {
   hip_check(hipSetDevice(op->device), "hipSetDevice");
   op->spike.next_round = -1;
   const SpikeTables &S = op->spike;
-  if ((S.k_end > S.k_begin || S.rounds > 0) && (S.has_lo || S.has_hi))
+  if ((S.k_end > S.k_begin || S.rounds > 0 || ghosts) && (S.has_lo || S.has_hi))
     hip_check(gdmk_launch_spike(op->p, x_local, op->layout.plane_size,
                                 (int64_t)op->layout.ghost_planes_below * op->layout.plane_size, S.n_planes, S.has_lo,
-                                S.has_hi, S.VW, S.S, S.k_begin, S.k_end, 0, 0, S.rounds > 0 ? S.G0 : nullptr,
-                                op->stream),
+                                S.has_hi, S.VW, S.S, S.k_begin, S.k_end, ghosts ? 2 : 0, 0,
+                                S.rounds > 0 ? S.G0 : nullptr, op->stream),
               "spike");
   return GDM_OK;
   GDM_GUARD_END

@@ -30,6 +30,7 @@ struct StencilArgs {
   // Toeplitz interiors exist (N >= 2p + 3) per axis
   int x_toep, y_toep, z_toep;
   double sx;        // h_y beta_x
+  double cxs[19];   // v8: sx bhat[k] (the x-sweep's B band with the scale folded in)
   double cy[19];    // h_x beta_y bhat[k]
   // x: wall-column corrections [2(p+1)][2(2p+1)]: ((M_x row - [x_toep] h_x mhat) / h_x,
   //    h_y (B_x row - [x_toep] beta_x bhat)); slot x for x < x_corr_left, slot p+1+j

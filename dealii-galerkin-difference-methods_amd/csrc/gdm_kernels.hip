@@ -51,6 +51,18 @@
 #ifndef GDM_STENCIL_ST_NT
 #define GDM_STENCIL_ST_NT 1
 #endif
+#ifndef GDM_EXP_BSTORE
+#define GDM_EXP_BSTORE 1
+#endif
+#ifndef GDM_EXP_MULFIRST
+#define GDM_EXP_MULFIRST 1
+#endif
+#ifndef GDM_EXP_SXFOLD
+#define GDM_EXP_SXFOLD 1
+#endif
+#ifndef GDM_EXP_HALFG
+#define GDM_EXP_HALFG 1
+#endif
 #if GDM_STENCIL_ST_NT
 #define GDM_STENCIL_STORE(p, v) __builtin_nontemporal_store((v), (p))
 #else
@@ -141,6 +153,7 @@ typedef double dpair __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) dpair ldouble2;
 typedef __attribute__((address_space(3))) const double lcdouble;
 typedef __attribute__((address_space(3))) const dpair lcdouble2;
+typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
 // compiler-only fence: no memory access and no instruction crosses it, so the
 // scheduler cannot hoist all LDS reads of a sweep to its top (their registers
 // would overlap the accumulator ring)
@@ -157,6 +170,7 @@ struct Tile7 {
   bool yedge;  // v8: the tile has rows next to a y wall
   int ry0;     // v8 y-wall tiles: first tile row of the column table (yb - y0)
   int lane, wv, x0, y0, zc0, zc1, zs, ze, zend;
+  unsigned ooff;  // v8 consumers: byte offset of the lane's first output row in an output plane
   // x wall columns inside this tile: nl from the left wall, nr from column rs on
   int nl, rs, ncw;
 };
@@ -988,17 +1002,82 @@ __device__ __forceinline__ void xcalc8(const StencilArgs &a, const double (&w)[G
             V[j / 2].y = fma(IR::m[k], w[j + k + 1], V[j / 2].y);
         } else {
           V[j].x = fma(IR::m[k], w[j + k + 1], V[j].x);
+#if GDM_EXP_SXFOLD
+          // B* = sx bhat * u with the scale folded into the run-time band
+          // cxs = sx bhat (first half in SGPRs, hcoef), c[p] == 0 skipped
+          if (BK != 1 || k != P) V[j].y = fma(hcoef<P, BK>(a.cxs, k), w[j + k + 1], V[j].y);
+#else
           // the antisymmetric interior band has c[p] == 0: no FMA for it
           if constexpr (BK == 1) {
             if (IR::c[k] != 0.0) V[j].y = fma(IR::c[k], w[j + k + 1], V[j].y);
           }
           if constexpr (BK == 2) V[j].y = fma(IR::l[k], w[j + k + 1], V[j].y);
+#endif
         }
       }
   }
+#if !GDM_EXP_SXFOLD
   if constexpr (BK != 0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) V[j].y *= a.sx;
+  }
+#endif
+}
+
+// The last row group of a tile when it holds at most 2 rows (p = 5: rows
+// 40, 41 of 42): 2 rows x 64 x, two consecutive x per lane, so the wave
+// issues half the FMAs of a 4-row group (whose rows 42, 43 would be discarded)
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void xsweep8_half(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  using IR = InteriorRows<P>;
+  constexpr int W = G::W, RL = G::RL, NW2 = 2 * P + 4;
+  const int rr = t.lane >> 5, q = t.lane & 31;
+  const int r = 4 * g + rr;
+  double w[NW2];
+  lcdouble2 *wp = (lcdouble2 *)(us + r * RL + 2 * q);
+#pragma unroll
+  for (int i = 0; i < NW2 / 2; ++i) {
+    const dpair v = wp[i];
+    w[2 * i] = v.x;
+    w[2 * i + 1] = v.y;
+  }
+  dpair V[2] = {dpair{0.0, 0.0}, dpair{0.0, 0.0}};
+#pragma unroll
+  for (int k = 0; k < W; ++k)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if constexpr (BK == 0) {
+        if (j == 0)
+          V[0].x = fma(IR::m[k], w[j + k + 1], V[0].x);
+        else
+          V[0].y = fma(IR::m[k], w[j + k + 1], V[0].y);
+      } else {
+        V[j].x = fma(IR::m[k], w[j + k + 1], V[j].x);
+#if GDM_EXP_SXFOLD
+        if (BK != 1 || k != P) V[j].y = fma(hcoef<P, BK>(a.cxs, k), w[j + k + 1], V[j].y);
+#else
+        if constexpr (BK == 1) {
+          if (IR::c[k] != 0.0) V[j].y = fma(IR::c[k], w[j + k + 1], V[j].y);
+        }
+        if constexpr (BK == 2) V[j].y = fma(IR::l[k], w[j + k + 1], V[j].y);
+#endif
+      }
+    }
+#if !GDM_EXP_SXFOLD
+  if constexpr (BK != 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) V[j].y *= a.sx;
+  }
+#endif
+  if (r < G::UR) {
+    if constexpr (BK != 0) {
+      ldouble2 *row = (ldouble2 *)(t.ab0 + r * G::ABRS);
+      row[G::sw(2 * q)] = V[0];
+      row[G::sw(2 * q + 1)] = V[1];
+    } else {
+      *(ldouble2 *)(t.ab0 + r * G::TX + 2 * q) = V[0];
+    }
   }
 }
 
@@ -1182,8 +1261,13 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
     for (int ps = 0; ps < G::NPASS; ++ps) {
       const int g = t.wv + ps * NP;
       if (g < G::NG) {
-        xsweep8<P, R, NC, NP, BK>(a, tt, u[slot], g, V1);
-        write_ab8<P, R, NC, NP, BK>(tt, g, V1);
+        constexpr bool half_last = GDM_EXP_HALFG && (G::UR - 4 * (G::NG - 1) <= 2);
+        if (half_last && g == G::NG - 1) {
+          xsweep8_half<P, R, NC, NP, BK>(a, tt, u[slot], g);
+        } else {
+          xsweep8<P, R, NC, NP, BK>(a, tt, u[slot], g, V1);
+          write_ab8<P, R, NC, NP, BK>(tt, g, V1);
+        }
         if (t.ncw > 0) {
           XWall<P, BK> xw0;
           xwall8_calc<P, R, NC, NP, BK>(tt, u[slot], g, xpre, xw0);
@@ -1292,6 +1376,11 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
       if constexpr (G::NYW == 1) sync_signal(t.sync + SY_YWR);
     }
     sync_signal(t.sync + SY_FREE + bs);
+    // MF: the slot of output zz + p (k = 2p) was retired by the previous
+    // plane; its first term overwrites it (a multiply instead of a zeroing
+    // move + FMA).  Outputs whose first plane zz + p - 2p precedes the chunk
+    // start keep the ring's initial zeros and only ever see FMAs.
+    constexpr bool MF = GDM_EXP_MULFIRST;
     if constexpr (!WALL) {
       // interior z column: out += mhat[k] E + zd[k] D with zd = dint dhat[2p - k]
       // (the scale folded into the coefficients; zd[p] = 0 for advection)
@@ -1299,14 +1388,17 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
       for (int k = 0; k < W; ++k) {
         GDM_FENCE();
         const int slot = (JP - P + k + 2 * W) % W;
+        const bool first = MF && k == W - 1;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
+          const double c0 = first ? 0.0 : acc[slot][j];
           if constexpr (BK == 0)
-            acc[slot][j] = fma(hcoef<P, BK>(a.zd, k), D[j], acc[slot][j]);
+            acc[slot][j] = first ? hcoef<P, BK>(a.zd, k) * D[j] : fma(hcoef<P, BK>(a.zd, k), D[j], c0);
           else if (zband<P, BK>(k) == 0.0)
-            acc[slot][j] = fma(IR::m[k], E[j], acc[slot][j]);
+            acc[slot][j] = first ? IR::m[k] * E[j] : fma(IR::m[k], E[j], c0);
           else
-            acc[slot][j] = fma(IR::m[k], E[j], fma(hcoef<P, BK>(a.zd, k), D[j], acc[slot][j]));
+            acc[slot][j] =
+                fma(IR::m[k], E[j], first ? hcoef<P, BK>(a.zd, k) * D[j] : fma(hcoef<P, BK>(a.zd, k), D[j], c0));
         }
       }
     } else {
@@ -1319,12 +1411,13 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
         GDM_FENCE();
         const dpair nxt = zc[k + 1 < W ? k + 1 : k];
         const int slot = (JP - P + k + 2 * W) % W;
+        const bool first = MF && k == W - 1;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
           if constexpr (BK == 0)
-            acc[slot][j] = fma(cur.y, D[j], acc[slot][j]);
+            acc[slot][j] = first ? cur.y * D[j] : fma(cur.y, D[j], acc[slot][j]);
           else
-            acc[slot][j] = fma(cur.x, E[j], fma(cur.y, D[j], acc[slot][j]));
+            acc[slot][j] = fma(cur.x, E[j], first ? cur.y * D[j] : fma(cur.y, D[j], acc[slot][j]));
         }
         cur = nxt;
       }
@@ -1342,18 +1435,35 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
   const int zo = zz - P;
   if (zo >= t.zc0 && zo < t.zc1) {
     const int Nx = a.Nx, x = t.x0 + t.lane;
-    double *orow = a.dst + ((int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) + (ybase - a.out_y0)) * Nx + x;
-    if (full) {
+#if GDM_EXP_BSTORE
+    // buffer stores: the plane's base in the resource (scalar), the lane's
+    // row offset a per-wave constant, row j's offset in soffset -- no 64-bit
+    // per-lane address arithmetic per plane (non-temporal, cpol 2 = nt);
+    // partial tiles mask rows (wave-uniform) and lanes
+    const double *pb = a.dst + (int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) * Nx;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)pb, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-      for (int j = 0; j < R; ++j) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
-    } else {
+    for (int j = 0; j < R; ++j)
+      if (full || (ybase + j < a.out_y1 && x < Nx))
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, acc[rslot][j]), rs, t.ooff, j * Nx * 8, 2);
+#else
+    {
+      double *orow = a.dst + ((int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) + (ybase - a.out_y0)) * Nx + x;
+      if (full) {
 #pragma unroll
-      for (int j = 0; j < R; ++j)
-        if (x < Nx && ybase + j < a.out_y1) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
+        for (int j = 0; j < R; ++j) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          if (x < Nx && ybase + j < a.out_y1) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
+      }
     }
+#endif
   }
+  if constexpr (!GDM_EXP_MULFIRST) {
 #pragma unroll
-  for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
+    for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
+  }
 }
 
 template <int JP, int P, int R, int NC, int NP, int BK, int PF, bool WALL, bool YW>
@@ -1395,10 +1505,11 @@ __device__ __forceinline__ void consumer8_loop(const StencilArgs &a, const Tile7
 }
 
 template <int P, int R, int NC, int NP, int BK, int PF>
-__device__ __forceinline__ void consumer8(const StencilArgs &a, const Tile7 &t) {
+__device__ __forceinline__ void consumer8(const StencilArgs &a, Tile7 t) {
   using G = Geom8<P, R, NC, NP, BK>;
   const int ybase = t.y0 + t.cw * R;
   const bool full = (t.x0 + G::TX <= a.Nx) && (ybase + R <= a.out_y1);
+  t.ooff = (unsigned)(((ybase - a.out_y0) * a.Nx + t.x0 + t.lane) * 8);
   // edge tiles (rows next to a y wall) wait for the producers' y-wall
   // corrections every plane: their own copy of the loop keeps that out of the
   // hot block of the other tiles

@@ -83,7 +83,8 @@ hipError_t gdmk_launch_periodic(double *v, const int64_t N[3], int d, int mode, 
 // [k_begin, k_end): x_k -= VW[k][0:p] . t + VW[k][p:2p] . b (mode 0; G0 != NULL:
 // the saved edge planes are restored first).  mode 1 (refinement round):
 // the owned first / last p planes become g_first - V[0:p] t / g_last - W[n-p:n] b
-// with g saved to G0 [2p][plane_size] at round 0
+// with g saved to G0 [2p][plane_size] at round 0.  mode 2: mode 0, and b / t
+// overwrite the ghost planes below / above (the neighbours' edge planes of x)
 hipError_t gdmk_launch_spike(int p, double *x_local, int64_t plane_size, int64_t own_off, int n_planes, int has_lo,
                              int has_hi, const double *VW, const double *S, int k_begin, int k_end, int mode,
                              int round, double *G0, hipStream_t st);

@@ -167,7 +167,11 @@ __global__ void __launch_bounds__(256) vmul_kernel(int64_t n, const double *__re
 // far-spike couplings evaluated at the current interface values:
 //   first p planes: g_first - V[0:p] t,  last p planes: g_last - W[n-p:n] b;
 // the caller then exchanges ghost planes again.  mode 0 with G0 != NULL
-// restores the saved edge planes before the update.
+// restores the saved edge planes before the update.  mode 2 = mode 0 and the
+// interface unknowns b / t (the lower neighbour's last p planes, the upper
+// neighbour's first p planes of x) also replace the ghost planes: x_local is
+// then a valid local vector of x without another exchange (the one-exchange
+// RK stage, gdm_mass_solve_interface_ghosts).
 template <int P>
 __global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps, int64_t own_off, int n, int has_lo,
                                                     int has_hi, const double *__restrict__ VW,
@@ -235,6 +239,13 @@ __global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps,
         xo[(int64_t)(n - P + a) * ps] = G0[(int64_t)(P + a) * ps + i];
       }
     }
+    if (mode == 2) {
+#pragma unroll
+      for (int a = 0; a < P; ++a) {
+        if (has_lo) xo[(int64_t)(a - P) * ps] = b[a];
+        if (has_hi) xo[(int64_t)(n + a) * ps] = t[a];
+      }
+    }
     for (int k = k_begin; k < k_end; ++k) {
       const double *vw = VW + (size_t)k * 2 * P;
       double c = 0.0;
@@ -253,6 +264,7 @@ extern "C" hipError_t gdmk_launch_spike(int p, double *x_local, int64_t ps, int6
                                        int has_hi, const double *VW, const double *S, int k_begin, int k_end,
                                        int mode, int round, double *G0, hipStream_t st) {
   if (ps <= 0 || (mode == 0 && !G0 && k_end <= k_begin)) return hipSuccess;
+  if (mode == 2 && !has_lo && !has_hi && !G0 && k_end <= k_begin) return hipSuccess;
   const unsigned blocks = (unsigned)std::min<int64_t>((ps + 255) / 256, 4096);
 #define GDM_SPIKE(PP)                                                                                           \
   case PP:                                                                                                      \

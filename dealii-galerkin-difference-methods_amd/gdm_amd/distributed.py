@@ -223,14 +223,17 @@ class SlabMassSolve:
     `rounds` None asks gdm_mass_spike_rounds for the operator's mesh (the C
     ABI refuses an interface call whose rounds did not all run)."""
 
-    def __init__(self, op, halo, rounds=None):
+    def __init__(self, op, halo, rounds=None, ghosts=False):
         if rounds is None:
             from . import _capi
 
             rounds = _capi.mesh_spike_rounds(op.mesh)
-        self.op, self.halo, self.rounds = op, halo, int(rounds)
+        self.op, self.halo, self.rounds, self.ghosts = op, halo, int(rounds), bool(ghosts)
 
     def solve(self, rhs_owned, x_local):
+        """ghosts=True: the ghost planes of x_local end up holding the
+        neighbours' edge planes of the result (gdm_mass_solve_interface_ghosts).
+        rhs_owned may be the owned view of x_local (in place)."""
         x_owned = self.op.owned_view(x_local)
         self.op.mass_solve_slab(rhs_owned, x_owned)
         if self.halo is not None:
@@ -239,8 +242,106 @@ class SlabMassSolve:
             self.op.mass_solve_interface_round(x_local, k)
             if self.halo is not None:
                 self.halo.exchange(x_local)
-        self.op.mass_solve_interface(x_local)
+        if self.ghosts:
+            self.op.mass_solve_interface_ghosts(x_local)
+        else:
+            self.op.mass_solve_interface(x_local)
         return x_owned
+
+
+RK4_A = (0.5, 0.5, 1.0)  # a_{s+1,s}
+RK4_B = (1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0)
+RK4_C = (0.0, 0.5, 0.5, 1.0)
+
+
+class SlabRK4:
+    """The advection problem's RK4 step (advection/problem.h:62-94: per stage
+    update_ghost_values + compute_rhs, stiffness.h:343-605, and the mass
+    solve, problem.h:236-267) on z-slab ranks with the exact distributed mass
+    inverse (SPIKE).  `ops` are rank operators evaluated in lockstep -- one per
+    process over torch.distributed, or several in one process for the tests --
+    and `exchange(vectors)` fills the ghost planes of each rank's local vector
+    (HaloExchange.exchange for one rank per process).
+
+    one_exchange=False: the reference's two exchanges per stage -- the stage
+    vector's ghost planes before the stencil and the SPIKE planes of the solve.
+    one_exchange=True: the SPIKE interface systems already give each rank the
+    neighbours' edge planes of k (gdm_mass_solve_interface_ghosts), so k is a
+    valid local vector; the low-storage updates acc = acc + h b_s k, Y = y +
+    h a k and the last stage's y = acc + h b_3 k then run over the whole local
+    vectors and keep the ghost planes of y, acc and Y current: the stage's
+    stencil needs no exchange, one per stage remains (+ the refinement rounds
+    of thin slabs).  The ghost planes then carry the neighbours' values as the
+    interface solution gives them (<= 1e-15 relative apart from the owner's,
+    the truncation of the interface systems); `resync` > 0 exchanges y's ghost
+    planes every `resync` steps.
+
+    The inflow data of a built-in boundary function (fn_kind, fn_params) are
+    computed by the engine per stage (gdm_apply_bc_fn); fn_kind None: no inflow
+    data.  State: self.y[r] (local vectors); the owned values are
+    ops[r].owned_view(self.y[r])."""
+
+    def __init__(self, ops, exchange, fn_kind=None, fn_params=(), one_exchange=True, rounds=None, resync=0):
+        from . import _capi
+
+        self.ops, self.exchange = list(ops), exchange
+        self.fn, self.prm = fn_kind, list(fn_params)
+        self.one = bool(one_exchange)
+        self.rounds = _capi.mesh_spike_rounds(self.ops[0].mesh) if rounds is None else int(rounds)
+        if self.rounds < 0:
+            raise ValueError("SlabRK4: the partition is too thin for the SPIKE mass inverse")
+        self.resync, self.steps = int(resync), 0
+        self.y = [op.new_vector(True) for op in self.ops]
+        self._acc = [op.new_vector(True) for op in self.ops]
+        self._Y = [op.new_vector(True) for op in self.ops]
+        self._k = [op.new_vector(True) for op in self.ops]
+
+    def set_solution(self, owned_values):
+        """owned_values[r]: rank r's owned DoF values; the ghost planes are
+        exchanged once"""
+        for op, y, v in zip(self.ops, self.y, owned_values):
+            y.zero_()
+            op.owned_view(y).copy_(v)
+        self.exchange(self.y)
+
+    def _rhs(self, t, h, s, stage):
+        for op, src, k in zip(self.ops, stage, self._k):
+            dst = op.owned_view(k)
+            if self.fn is None:
+                op.apply(src, dst)
+            else:
+                alpha, t_k = (0.0, t) if s == 0 else (h * RK4_A[s - 1], t + RK4_C[s - 1] * h)
+                op.apply_bc_fn(src, dst, self.fn, self.prm, t, alpha, t_k)
+        for op, k in zip(self.ops, self._k):
+            own = op.owned_view(k)
+            op.mass_solve_slab(own, own)
+        self.exchange(self._k)
+        for rnd in range(self.rounds):
+            for op, k in zip(self.ops, self._k):
+                op.mass_solve_interface_round(k, rnd)
+            self.exchange(self._k)
+        for op, k in zip(self.ops, self._k):
+            if self.one:
+                op.mass_solve_interface_ghosts(k)
+            else:
+                op.mass_solve_interface(k)
+
+    def step(self, t, h):
+        stage = self.y
+        for s in range(4):
+            if not self.one:
+                self.exchange(stage)  # update_ghost_values of the stage vector (stiffness.h:343)
+            self._rhs(t, h, s, stage)
+            last = s == 3
+            for op, k, y, acc, Y in zip(self.ops, self._k, self.y, self._acc, self._Y):
+                if last:
+                    op.rk_update(h * RK4_B[s], k, acc, y)
+                else:
+                    op.rk_update(h * RK4_B[s], k, y if s == 0 else acc, acc, h * RK4_A[s], y, Y)
+            stage = self._Y
+        self.steps += 1
+        if self.one and self.resync > 0 and self.steps % self.resync == 0:
+            self.exchange(self.y)
 
 
 SPIKE_TOL = 1e-15

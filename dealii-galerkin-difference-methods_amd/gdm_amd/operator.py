@@ -260,6 +260,17 @@ class GdmOperator:
         check(self.lib.gdm_mass_solve_interface(self.h, _ptr(x_local)), "gdm_mass_solve_interface")
         return x_local
 
+    def mass_solve_interface_ghosts(self, x_local):
+        """mass_solve_interface, and the ghost planes of x_local become the
+        interface solution (the neighbours' edge planes of M^-1 rhs,
+        gdm_mass_solve_interface_ghosts): x_local is a valid local vector
+        without another exchange"""
+        if x_local.numel() != self.n_local:
+            raise GdmError("mass_solve_interface_ghosts: x has %d entries, expected n_local %d"
+                           % (x_local.numel(), self.n_local))
+        check(self.lib.gdm_mass_solve_interface_ghosts(self.h, _ptr(x_local)), "gdm_mass_solve_interface_ghosts")
+        return x_local
+
     def error_norms(self, u_local, fn_kind, params, t, cell_errors=None):
         """(Linf, L1, L2) of u - f(t) over QGauss(p+1) on the owned cells
         (advection/problem.h:269-425 postprocess, volume part); cell_errors

@@ -3,7 +3,7 @@
 // (gdm/hip/operators.h), in the shape of
 // applications/advection/advection-app.cc:86-154 + problem.h:31-102.
 //
-//   advection_app DIM P N STEPS CFL OUT [DEVICE] [DEVBC] [NRANKS]
+//   advection_app DIM P N STEPS CFL OUT [DEVICE] [DEVBC] [NRANKS] [EXCHANGES]
 //
 // Manufactured solution u(x, t) = prod_d sin(2 pi (x_d - a_d t) + 0.3 d) on
 // [0, 1]^dim with a = (1, 0.15, -0.05) (prototypes/advection_01_gdm.cc:37-41);
@@ -18,6 +18,8 @@
 // and dots through GDM::HIP::ThreadGroup (an MPI communicator's role), the
 // distributed exact mass inverse (SPIKE) when the slabs are thick enough, else
 // the distributed Jacobi CG; OUT holds the ranks' owned values in rank order.
+// EXCHANGES (SPIKE runs): 1 = one ghost exchange per RK stage (default,
+// Parameters::one_exchange_per_stage), 2 = the reference's two.
 // With DEVBC the final errors against the exact solution are computed on the
 // device (AdvectionProblem::postprocess -> gdm_error_norms) and printed in the
 // reference's postprocess format (time, L2, L1, Linf).
@@ -85,11 +87,11 @@ GDM::HIP::Parameters<dim> make_params(int p, int n, double cfl, int device, int 
 }
 
 template <int dim>
-int run(int p, int n, int steps, double cfl, const char *out, int device, int devbc, int n_ranks) {
+int run(int p, int n, int steps, double cfl, const char *out, int device, int devbc, int n_ranks, int exchanges) {
   std::vector<double> u;
   unsigned int done = 0;
   std::array<double, 6> norms{{-1.0, -1.0, -1.0, 0.0, 0.0, 0.0}};
-  bool spike = false;
+  bool spike = false, one_ex = false;
   if (n_ranks <= 1) {
     GDM::HIP::AdvectionProblem<dim> problem(make_params<dim>(p, n, cfl, device, devbc));
     done = problem.run(steps);
@@ -122,6 +124,7 @@ int run(int p, int n, int steps, double cfl, const char *out, int device, int de
           GDM::HIP::Parameters<dim> params = make_params<dim>(p, n, cfl, device, devbc);
           params.n_ranks = n_ranks;
           params.rank = r;
+          params.one_exchange_per_stage = exchanges != 2;
           GDM::HIP::ThreadGroup::Rank comm(group, r, mesh);
           GDM::HIP::AdvectionProblem<dim> problem(params, &comm);
           steps_done[r] = problem.run(steps);
@@ -131,6 +134,7 @@ int run(int p, int n, int steps, double cfl, const char *out, int device, int de
             if (r == 0) norms = e;
           }
           if (r == 0) spike = problem.used_spike_solve();
+          if (r == 0) one_ex = problem.used_one_exchange();
         } catch (const std::exception &e) {
           errors[r] = e.what();
           std::fprintf(stderr, "rank %d: %s\n", r, e.what());
@@ -145,6 +149,7 @@ int run(int p, int n, int steps, double cfl, const char *out, int device, int de
   for (double v : u) s += v * v;
   std::printf("steps %u  |u|_2 %.15e\n", done, std::sqrt(s));
   if (n_ranks > 1) std::printf("mass solve: %s\n", spike ? "spike" : "cg");
+  if (n_ranks > 1) std::printf("exchanges per stage: %d\n", one_ex ? 1 : 2);
   if (devbc)  // the reference's postprocess line (problem.h:427-433): counter, time, L2, L1, Linf
     std::printf("%5d %8.5f %14.8e %14.8e %14.8e\n", 0, time_of(done, n, cfl), norms[2], norms[1], norms[0]);
   std::ofstream f(out, std::ios::binary);
@@ -164,11 +169,12 @@ int main(int argc, char **argv) {
   const int device = argc > 7 ? std::atoi(argv[7]) : 0;
   const int devbc = argc > 8 ? std::atoi(argv[8]) : 0;
   const int n_ranks = argc > 9 ? std::atoi(argv[9]) : 1;
+  const int exchanges = argc > 10 ? std::atoi(argv[10]) : 1;
   try {
     switch (dim) {
-      case 1: return run<1>(p, n, steps, cfl, argv[6], device, devbc, n_ranks);
-      case 2: return run<2>(p, n, steps, cfl, argv[6], device, devbc, n_ranks);
-      case 3: return run<3>(p, n, steps, cfl, argv[6], device, devbc, n_ranks);
+      case 1: return run<1>(p, n, steps, cfl, argv[6], device, devbc, n_ranks, exchanges);
+      case 2: return run<2>(p, n, steps, cfl, argv[6], device, devbc, n_ranks, exchanges);
+      case 3: return run<3>(p, n, steps, cfl, argv[6], device, devbc, n_ranks, exchanges);
       default: std::fprintf(stderr, "dim must be 1, 2 or 3\n"); return 2;
     }
   } catch (const GDM::HIP::Error &e) {

@@ -78,6 +78,17 @@ struct Parameters {
   // same bits for block(1); block(0) of the solution is then not maintained
   // (initialize_time_step overwrites it every step, problem.h:88-90)
   bool boundary_in_faces = true;
+  // n_ranks > 1 with the exact SPIKE mass inverse: ONE exchange per RK stage.
+  // The interface systems give each rank the neighbours' edge planes of k
+  // (gdm_mass_solve_interface_ghosts), the stage updates run over the local
+  // vectors, so y / acc / Y keep valid ghost planes and the stencil needs no
+  // update_ghost_values (advection/stiffness.h:343); the solve's exchange is
+  // the one left.  Ghost values then follow the neighbours' to the interface
+  // truncation (<= 1e-15 relative per stage); ghost_resync_steps > 0
+  // re-exchanges the solution's ghost planes every that many steps.  false:
+  // the reference's two exchanges per stage.
+  bool one_exchange_per_stage = true;
+  unsigned int ghost_resync_steps = 0;
 };
 
 // A device buffer of doubles allocated through the engine (gdm_malloc).
@@ -494,6 +505,22 @@ class MassMatrixOperator {
     check(gdm_mass_solve_interface(op, sp_x.get_values()), "gdm_mass_solve_interface");
     check(gdm_memcpy_d2d(op, x_owned, own, sizeof(double) * layout.n_owned), "gdm_memcpy_d2d");
   }
+  // x_local (engine-local layout) = M^-1 of its owned part, in place, with
+  // its ghost planes set to the neighbours' edge planes of the result from
+  // the interface systems (gdm_mass_solve_interface_ghosts): one exchange
+  // (+ the refinement rounds of thin slabs), no copy
+  void solve_spike_local(DeviceVector &x_local, Communicator &comm) const {
+    if (x_local.size() != (std::size_t)layout.n_local) throw Error("solve_spike_local: x must be a local vector");
+    if (sp_rounds < 0) sp_rounds = spike_rounds();
+    double *own = x_local.get_values() + layout.ghost_planes_below * layout.plane_size;
+    check(gdm_mass_solve_slab(op, own, own), "gdm_mass_solve_slab");
+    comm.update_ghost_values(op, x_local);
+    for (int k = 0; k < sp_rounds; ++k) {
+      check(gdm_mass_solve_interface_round(op, x_local.get_values(), k), "gdm_mass_solve_interface_round");
+      comm.update_ghost_values(op, x_local);
+    }
+    check(gdm_mass_solve_interface_ghosts(op, x_local.get_values()), "gdm_mass_solve_interface_ghosts");
+  }
   gdm_op *handle() const { return op; }
 
  private:
@@ -565,9 +592,23 @@ class AdvectionProblem {
     stiffness_matrix_operator.initialize_dof_vector(stage, !in_faces);
     if (params.n_ranks != 1) rhs_tmp.reinit(stiffness_matrix_operator.handle(), stiffness_matrix_operator.get_layout().n_owned);
     use_spike = params.n_ranks != 1 && mass_matrix_operator.spike_available();
+    one_exchange = use_spike && params.one_exchange_per_stage;
+    // the ghost planes of the solution once at the start (set_initial_condition
+    // interpolates them too); with one_exchange they are kept current by the
+    // local-vector updates from then on
+    if (one_exchange) comm->update_ghost_values(stiffness_matrix_operator.handle(), solution.block(1));
     // stage boundary values computed by the engine: g(t0) + alpha dg/dt(t_k)
     double t0 = 0.0, bc_alpha = 0.0, bc_tk = 0.0;
     const auto fu_rhs = [&](double time, BlockVector &y, BlockVector &result) {
+      if (one_exchange) {
+        // the stage vector's ghost planes are current: no update_ghost_values
+        if (in_faces)
+          stiffness_matrix_operator.compute_rhs_fn(result.block(1), y.block(1), t0, bc_alpha, bc_tk);
+        else
+          stiffness_matrix_operator.compute_rhs(result, y, time);
+        mass_matrix_operator.solve_spike_local(result.block(1), *comm);
+        return;
+      }
       if (in_faces) {
         if (params.n_ranks != 1 && params.overlap_exchange) {
           stiffness_matrix_operator.compute_rhs_fn_overlapped(result.block(1), y.block(1), t0, bc_alpha, bc_tk,
@@ -610,6 +651,8 @@ class AdvectionProblem {
       }
       time.advance_time();
       ++n;
+      if (one_exchange && params.ghost_resync_steps > 0 && n % params.ghost_resync_steps == 0)
+        comm->update_ghost_values(stiffness_matrix_operator.handle(), solution.block(1));
     }
     return n;
   }
@@ -624,6 +667,8 @@ class AdvectionProblem {
   const BlockVector &get_solution_vector() const { return solution; }
   // which multi-rank mass solve run() used: exact SPIKE or the Jacobi CG
   bool used_spike_solve() const { return use_spike; }
+  // whether run() did one exchange per stage (Parameters::one_exchange_per_stage)
+  bool used_one_exchange() const { return one_exchange; }
 
   // postprocess(time, solution) (problem.h:269-485), error part on the device:
   // {Linf, L1, L2, Linf_face, L1_face, L2_face} of u - exact_solution(time)
@@ -678,7 +723,7 @@ class AdvectionProblem {
   StiffnessMatrixOperator<dim> stiffness_matrix_operator;
   BlockVector solution;
   DeviceVector rhs_tmp;
-  bool use_spike = false;
+  bool use_spike = false, one_exchange = false;
 };
 
 }  // namespace HIP

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 13
+#define GDM_HIP_ABI_VERSION 14
 
 enum gdm_status {
   GDM_OK = 0,
@@ -245,6 +245,16 @@ int gdm_mass_spike_rounds(const gdm_mesh_desc *mesh, int *rounds);
 int gdm_mass_solve_slab(gdm_op *op, const double *rhs_owned, double *x_owned);
 int gdm_mass_solve_interface_round(gdm_op *op, double *x_local, int round);
 int gdm_mass_solve_interface(gdm_op *op, double *x_local);
+/* gdm_mass_solve_interface, and the ghost planes of x_local are overwritten
+ * with the interface solution -- the lower neighbour's last p planes and the
+ * upper neighbour's first p planes of M^-1 rhs, which each interface system
+ * yields on both ranks of the pair (ABI 14).  x_local is then a valid local
+ * vector of M^-1 rhs (ghosts equal to the neighbours' owned values to the
+ * truncation tolerance, <= 1e-15 relative): an RK stage that updates its
+ * local vectors over the ghost planes too (k, acc, y, Y in local layout)
+ * needs no update_ghost_values before the next stage's stencil
+ * (advection/stiffness.h:343) -- one exchange per stage, the SPIKE one. */
+int gdm_mass_solve_interface_ghosts(gdm_op *op, double *x_local);
 
 /* x_owned = M^-1 rhs_owned by SolverCG on the matrix-free mass operator with
  * ReductionControl(max_it, abs_tol, rel_tol) semantics, the solve of

@@ -88,3 +88,44 @@ def test_c3_eight_ranks_compute_rhs_and_spike_match_single_rank():
         op.mass_solve_interface(x)
     got = torch.cat([op.owned_view(x) for op, x in zip(ops, xs)])
     assert _rel(got, m_ref) < 1e-13
+
+
+def test_c3_eight_ranks_one_exchange_rk_step():
+    """VERDICT r5 item 4 at the C3 split: one RK4 step of the 512^3 p = 5
+    advection problem on 8 z-slab ranks (inflow data computed by the engine)
+    with one exchange per stage (SlabRK4 one_exchange: the stage's ghost
+    planes from the SPIKE interface solution) == the two-exchange stage
+    (update_ghost_values before compute_rhs + the solve's exchange), rel-L2
+    <= 1e-13.  Peak device memory ~10 GB."""
+    import gdm_amd
+    from gdm_amd.distributed import SlabRK4
+
+    sine = [1.0, 0.15, -0.05, 1.0, 1.0, 1.0, 0.3, 0.0, 0.7]
+    ops = [gdm_amd.GdmOperator(3, P, N_CELLS, 0.0, 1.0, "advection", params=A, rank=r, n_ranks=R) for r in range(R)]
+    ps = ops[0].layout["plane_size"]
+
+    def exchange(vs):
+        torch.cuda.synchronize()
+        for r, op in enumerate(ops):
+            L = op.layout
+            gb, ga, own = L["ghost_planes_below"], L["ghost_planes_above"], L["n_owned"] // ps
+            if r > 0 and gb:
+                Ln = ops[r - 1].layout
+                e = (Ln["ghost_planes_below"] + Ln["n_owned"] // ps) * ps
+                vs[r][:gb * ps] = vs[r - 1][e - gb * ps:e]
+            if r + 1 < R and ga:
+                Ln = ops[r + 1].layout
+                b = Ln["ghost_planes_below"] * ps
+                vs[r][(gb + own) * ps:(gb + own + ga) * ps] = vs[r + 1][b:b + ga * ps]
+
+    gen = torch.Generator("cuda").manual_seed(23)
+    u0 = [torch.rand(op.n_owned, dtype=torch.float64, device="cuda", generator=gen) - 0.5 for op in ops]
+    res = {}
+    for one_ex in (False, True):
+        rk = SlabRK4(ops, exchange, 2, sine, one_exchange=one_ex)
+        rk.set_solution(u0)
+        rk.step(0.0, 1e-3)
+        torch.cuda.synchronize()
+        res[one_ex] = torch.cat([op.owned_view(y) for op, y in zip(ops, rk.y)])
+        del rk
+    assert _rel(res[True], res[False]) < 1e-13

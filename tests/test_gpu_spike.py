@@ -114,3 +114,85 @@ def test_interface_refuses_skipped_or_out_of_order_rounds():
     from gdm_amd.distributed import SlabMassSolve
 
     assert SlabMassSolve(op, None).rounds == 1
+
+
+@pytest.mark.parametrize("dim,p,n,R", [(3, 5, (12, 10, 130), 2), (2, 3, (20, 150), 3), (1, 5, 400, 4),
+                                       (3, 7, (8, 9, 255), 8)])
+def test_interface_ghosts_give_the_neighbours_planes(dim, p, n, R):
+    """gdm_mass_solve_interface_ghosts (ABI 14): the owned part is bitwise
+    gdm_mass_solve_interface's, and the ghost planes hold the neighbours'
+    owned edge planes of M^-1 rhs (the interface solution both ranks of a
+    pair compute) to 1e-13 of the vector's max -- what the one-exchange RK
+    stage relies on (C4 at 8 ranks: after its refinement round)."""
+    import gdm_amd
+
+    rounds = gdm_amd._capi.mass_spike_rounds(dim, p, n, R)
+    one = gdm_amd.GdmOperator(dim, p, n, 0.0, 1.0, "mass")
+    r = torch.from_numpy(np.random.default_rng(5).uniform(-1, 1, one.n_owned)).cuda()
+    del one
+    ops = _ranks(gdm_amd, dim, p, n, R)
+    out = {}
+    for ghosts in (False, True):
+        xs = []
+        for op in ops:
+            a = op.layout["owned_plane_begin"] * op.layout["plane_size"]
+            x = op.new_vector(True)
+            op.mass_solve_slab(r[a:a + op.n_owned].contiguous(), op.owned_view(x))
+            xs.append(x)
+        torch.cuda.synchronize()
+        _exchange(ops, xs)
+        for k in range(rounds):
+            for op, x in zip(ops, xs):
+                op.mass_solve_interface_round(x, k)
+            torch.cuda.synchronize()
+            _exchange(ops, xs)
+        for op, x in zip(ops, xs):
+            (op.mass_solve_interface_ghosts if ghosts else op.mass_solve_interface)(x)
+        torch.cuda.synchronize()
+        out[ghosts] = xs
+    scale = max(float(x.abs().max()) for x in out[False])
+    for r_, op in enumerate(ops):
+        assert torch.equal(op.owned_view(out[True][r_]), op.owned_view(out[False][r_]))
+    # ghost planes == the neighbours' owned values
+    ref = [x.clone() for x in out[True]]
+    _exchange(ops, ref)
+    for x, y in zip(out[True], ref):
+        assert float((x - y).abs().max()) <= 1e-13 * scale
+
+
+@pytest.mark.parametrize("dim,p,n,R,kind", [(3, 5, (70, 40, 130), 3, "advection"), (2, 5, (90, 150), 4, "advection"),
+                                            (3, 7, (40, 33, 255), 8, "advection")])
+def test_one_exchange_rk_step_matches_two_exchange(dim, p, n, R, kind):
+    """SlabRK4 (gdm_amd.distributed): RK4 steps with one exchange per stage
+    (the stage's ghost planes from the SPIKE interface solution) == the
+    reference's two exchanges per stage (stiffness.h:343 + the solve's) to
+    1e-13, with the engine's inflow data (gdm_apply_bc_fn) -- and the
+    two-exchange path == the single-rank AdvectionProblem step to 1e-12."""
+    import gdm_amd
+    from gdm_amd.distributed import SlabRK4
+
+    a = (1.0, 0.15, -0.05)[:dim]
+    sine = [1.0, 0.15, -0.05, 1.0, 1.0, 1.0, 0.3, 0.0, 0.7]
+    one = gdm_amd.GdmOperator(dim, p, n, 0.0, 1.0, kind, params=a)
+    gen = torch.Generator(device="cuda").manual_seed(17)
+    u0 = torch.rand(one.n_owned, dtype=torch.float64, device="cuda", generator=gen) - 0.5
+    h, steps = 2e-3, 3
+    pr = gdm_amd.AdvectionProblem(one, 2, sine)
+    pr.u.copy_(u0)
+    for s in range(steps):
+        pr.step(s * h, h)
+    torch.cuda.synchronize()
+    single = pr.u.clone()
+    del pr, one
+    ops = [gdm_amd.GdmOperator(dim, p, n, 0.0, 1.0, kind, params=a, rank=r, n_ranks=R) for r in range(R)]
+    ps = ops[0].layout["plane_size"]
+    res = {}
+    for one_ex in (False, True):
+        rk = SlabRK4(ops, lambda vs: (torch.cuda.synchronize(), _exchange(ops, vs)), 2, sine, one_exchange=one_ex)
+        rk.set_solution([u0[op.layout["owned_plane_begin"] * ps:op.layout["owned_plane_end"] * ps] for op in ops])
+        for s in range(steps):
+            rk.step(s * h, h)
+        torch.cuda.synchronize()
+        res[one_ex] = torch.cat([op.owned_view(y) for op, y in zip(ops, rk.y)])
+    assert float(torch.linalg.norm(res[True] - res[False]) / torch.linalg.norm(res[False])) < 1e-13
+    assert float(torch.linalg.norm(res[False] - single) / torch.linalg.norm(single)) < 1e-12

@@ -374,6 +374,144 @@ class _NpSpikeOp:
         return x_local
 
 
+class _NpSlabRkOp(_NpSpikeOp):
+    """_NpSpikeOp plus what SlabRK4 calls on a rank operator: the slab's
+    compute_rhs (no inflow data) K = B_x (x) M_q + M_x (x) B_q (2D, outflow
+    traces folded into B, advection/stiffness.h:411-417, :520-529) from the
+    local vector's planes to the owned ones, the RK update, the interface with
+    ghost planes (gdm_mass_solve_interface_ghosts: b / t into the ghosts)."""
+
+    def __init__(self, p, n, world, rank, a):
+        super().__init__(2, p, n, world, rank)
+        m = O.Mesh(2, p, list(n))
+        B = [m.advection_outflow_B(d, a[d]) for d in range(2)]
+        self.Bs = [self._dense(band) for band in B]
+        L = self.L
+        self.lb = L["owned_plane_begin"] - L["ghost_planes_below"]
+        self.le = L["owned_plane_end"] + L["ghost_planes_above"]
+        self.n_local = L["n_local"]
+
+    @staticmethod
+    def _dense(band):
+        n, W = band.shape
+        p = (W - 1) // 2
+        A = np.zeros((n, n))
+        for i in range(n):
+            for k in range(W):
+                if 0 <= i - p + k < n:
+                    A[i, i - p + k] = band[i, k]
+        return A
+
+    def new_vector(self, local=True):
+        import torch
+
+        return torch.zeros(self.n_local if local else self.L["n_owned"], dtype=torch.float64)
+
+    def apply(self, src_local, dst_owned):
+        L, P = self.L, self.plane
+        pb, pe = L["owned_plane_begin"], L["owned_plane_end"]
+        U = src_local.numpy().reshape(-1, P)
+        Mq, Bq = self.Ms[1][pb:pe, self.lb:self.le], self.Bs[1][pb:pe, self.lb:self.le]
+        out = Mq @ U @ self.Bs[0].T + Bq @ U @ self.Ms[0].T
+        dst_owned.numpy()[:] = out.reshape(-1)
+        return dst_owned
+
+    def rk_update(self, beta, k, acc_in, acc_out, alpha=0.0, y=None, Y=None):
+        kv, ai = k.numpy(), acc_in.numpy().copy()
+        if Y is not None:
+            Y.numpy()[:] = y.numpy() + alpha * kv
+        acc_out.numpy()[:] = ai + beta * kv
+        return acc_out
+
+    def mass_solve_interface_ghosts(self, x_local):
+        p, P, r = self.p, self.plane, self.rank
+        gb = self.L["ghost_planes_below"]
+        own, V, W, b, t = self._interface(x_local)
+        if getattr(self, "G0", None) is not None:
+            own[:p], own[-p:] = self.G0
+            self.G0 = None
+        own -= V @ t + W @ b
+        a = x_local.numpy().reshape(-1, P)
+        n = own.shape[0]
+        if r > 0:
+            a[gb - p:gb] = b
+        if r + 1 < self.world:
+            a[gb + n:gb + n + p] = t
+        return x_local
+
+
+def _rk_worker(rank, world, port, p, n, a, steps, q):
+    import torch
+    import torch.distributed as dist
+    from gdm_amd.distributed import HaloExchange, SlabRK4
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        op = _NpSlabRkOp(p, n, world, rank, a)
+        halo = HaloExchange(n[1], world, rank, op.plane, p)
+        rounds = _capi.mass_spike_rounds(2, p, list(n), world)
+        m = O.Mesh(2, p, list(n))
+        u0 = np.sin(np.linspace(0.0, 7.0, m.n_dofs)) + 0.3 * np.cos(np.linspace(0.0, 23.0, m.n_dofs))
+        L = op.L
+        mine = torch.from_numpy(u0[L["owned_plane_begin"] * op.plane:L["owned_plane_end"] * op.plane].copy())
+        out = {}
+        for one in (False, True):
+            rk = SlabRK4([op], lambda vs: [halo.exchange(v) for v in vs], one_exchange=one, rounds=rounds)
+            rk.set_solution([mine])
+            for s in range(steps):
+                rk.step(0.01 * s, 0.01)
+            out[one] = op.owned_view(rk.y[0]).numpy().copy()
+        q.put((rank, L["owned_plane_begin"] * op.plane, out[False], out[True]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,p,n", [(2, 3, (6, 60)), (3, 5, (5, 90)), (4, 3, (4, 48))])
+def test_one_exchange_rk_matches_two_exchange_gloo(world, p, n):
+    """the RK4 step with ONE exchange per stage (the
+    stage vector's ghost planes maintained from the SPIKE interface solution,
+    updates over the local vectors) == the reference's two exchanges per stage
+    (update_ghost_values before compute_rhs, stiffness.h:343, + the solve's),
+    to 1e-13 after 6 steps, and both == the single-rank RK4 of
+    y' = M^-1 K y to 1e-12 -- SlabRK4 over gloo with a numpy test double of
+    the rank operator (4 ranks of 12 planes at p = 3: one refinement round)."""
+    import torch.multiprocessing as mp
+
+    a, steps = (0.8, -0.6), 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rk_worker, args=(r, world, port, p, n, a, steps, q)) for r in range(world)]
+    for p_ in procs:
+        p_.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p_ in procs:
+        p_.join(120)
+    assert all(p_.exitcode == 0 for p_ in procs), [p_.exitcode for p_ in procs]
+    m = O.Mesh(2, p, list(n))
+    two, one = np.zeros(m.n_dofs), np.zeros(m.n_dofs)
+    for _, off, v2, v1 in res:
+        two[off:off + len(v2)] = v2
+        one[off:off + len(v1)] = v1
+    assert np.linalg.norm(one - two) / np.linalg.norm(two) < 1e-13
+    # single-rank reference: classic RK4 of y' = M^-1 K y
+    d = _NpSlabRkOp(p, n, 1, 0, a)
+    Mi = np.kron(d.Ms[1], d.Ms[0])
+    K = np.kron(d.Ms[1], d.Bs[0]) + np.kron(d.Bs[1], d.Ms[0])
+    f = lambda y: np.linalg.solve(Mi, K @ y)  # noqa: E731
+    y = np.sin(np.linspace(0.0, 7.0, m.n_dofs)) + 0.3 * np.cos(np.linspace(0.0, 23.0, m.n_dofs))
+    h = 0.01
+    for _ in range(steps):
+        k1 = f(y)
+        k2 = f(y + 0.5 * h * k1)
+        k3 = f(y + 0.5 * h * k2)
+        k4 = f(y + h * k3)
+        y = y + h / 6 * k1 + h / 3 * k2 + h / 3 * k3 + h / 6 * k4
+    assert np.linalg.norm(two - y) / np.linalg.norm(y) < 1e-12
+
+
 def _spike_worker(rank, world, port, dim, p, n, q):
     import torch
     import torch.distributed as dist
