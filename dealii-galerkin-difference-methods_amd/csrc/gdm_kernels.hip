@@ -60,6 +60,9 @@
 #ifndef GDM_EXP_SXFOLD
 #define GDM_EXP_SXFOLD 1
 #endif
+#ifndef GDM_EXP_SLEEP
+#define GDM_EXP_SLEEP 1
+#endif
 #ifndef GDM_EXP_HALFG
 #define GDM_EXP_HALFG 1
 #endif
@@ -894,11 +897,11 @@ __device__ __forceinline__ void sync_wait(lu32 *c, unsigned target) {
       "v_readfirstlane_b32 %1, %0\n\t"
       "s_cmp_ge_u32 %1, %3\n\t"
       "s_cbranch_scc1 2f\n\t"
-      "s_sleep 1\n\t"
+      "s_sleep %4\n\t"
       "s_branch 1b\n"
       "2:"
       : "=&v"(v), "=&s"(sv)
-      : "v"((unsigned)(uintptr_t)c), "s"(target)
+      : "v"((unsigned)(uintptr_t)c), "s"(target), "n"(GDM_EXP_SLEEP)
       : "memory", "scc");
 }
 
