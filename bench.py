@@ -318,12 +318,16 @@ def c4_rank_slab(steps=10, n_ranks=8, rank=3):
 def c3_rank_slab(steps=10, n_ranks=8, rank=3):
     """C3 at its named 8-GPU split, one rank's share on this GPU: rank 3 of 8
     of the 512^3 p = 5 advection grid (system.h:720-757: 64 owned + 2 x 5
-    ghost planes).  compute_rhs is timed as apply_overlapped runs it at N = 8
-    (advection/stiffness.h:343 update_ghost_values overlapped with the planes
-    that need no ghosts): the interior planes, the 2 x p edge planes, the
-    inflow data; the exchange itself needs a second GPU and is not part of
-    this figure.  The mass inverse is the distributed exact one of that rank
-    (truncated SPIKE: slab solve + interface correction, problem.h:236-267)."""
+    ghost planes).  compute_rhs_ms: the stage's compute_rhs of the
+    one-exchange RK (SlabRK4 / the C++ one_exchange_per_stage: the ghost
+    planes are current, one launch over the owned planes with the inflow
+    data); compute_rhs_overlapped_ms: as apply_overlapped runs it when the
+    stage vector is exchanged first (advection/stiffness.h:343
+    update_ghost_values overlapped with the planes that need no ghosts: the
+    interior planes, the 2 x p edge planes, the inflow data).  The exchanges
+    need a second GPU and are not part of these figures.  The mass inverse is
+    the distributed exact one of that rank (truncated SPIKE: slab solve +
+    interface correction with the ghost planes written, problem.h:236-267)."""
     import torch
     from gdm_amd import GdmOperator, _capi
     from gdm_amd.distributed import apply_overlapped
@@ -351,6 +355,10 @@ def c3_rank_slab(steps=10, n_ranks=8, rank=3):
         return e0.elapsed_time(e1) / steps
 
     whole = timed(lambda: apply_overlapped(op, None, u, v, bc if op.n_bc_points else None))
+    # the one-exchange RK stage (SlabRK4, C++ one_exchange_per_stage): the
+    # stage vector's ghost planes are current when the stencil starts, so
+    # compute_rhs is one launch over all owned planes (no overlap split)
+    single = timed(lambda: op.apply(u, v, bc if op.n_bc_points else None))
     interior = timed(lambda: op.apply_planes(u, v, lo, hi))
 
     def edges():  # both edge ranges in one launch, as apply_overlapped runs them
@@ -365,7 +373,7 @@ def c3_rank_slab(steps=10, n_ranks=8, rank=3):
         op.mass_solve_slab(r, op.owned_view(x))
         for k in range(rounds):
             op.mass_solve_interface_round(x, k)
-        op.mass_solve_interface(x)
+        op.mass_solve_interface_ghosts(x)
 
     spike = timed(solve)
     N = op.n_owned
@@ -374,10 +382,12 @@ def c3_rank_slab(steps=10, n_ranks=8, rank=3):
         "workload": "C3 rank %d of %d: 512^2 x %d owned planes + %d + %d ghost planes, p=5 advection"
                     % (rank, n_ranks, pe - pb, L["ghost_planes_below"], L["ghost_planes_above"]),
         "n_dofs_rank": N,
-        "compute_rhs_ms": whole,
+        "compute_rhs_ms": single,
+        "compute_rhs_overlapped_ms": whole,
         "interior_planes_ms": interior,
         "edge_planes_ms": edge,
-        "stencil_frac": BYTES_PER_DOF * N / (whole * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "stencil_frac": BYTES_PER_DOF * N / (single * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "stencil_frac_overlapped": BYTES_PER_DOF * N / (whole * 1e-3) / 1e9 / HBM_PEAK_GBS,
         "interior_frac": BYTES_PER_DOF * n_int / (interior * 1e-3) / 1e9 / HBM_PEAK_GBS,
         "spike_solve_ms": spike,
         "spike_rounds": rounds,

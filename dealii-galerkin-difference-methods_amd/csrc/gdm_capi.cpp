@@ -1173,7 +1173,8 @@ bool mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
     return v3 && t.l3 && span_ok && (q.dir_kind == 1 || (q.len % 2 == 0 && aligned));
   };
   bool segmented = false;
-  for (const Pass &q : passes) segmented = segmented || (v3 && tab[q.ax].l3 && (q.n_lines + 63) / 64 < 512);
+  for (const Pass &q : passes)
+    segmented = segmented || (v3 && tab[q.ax].l3 && (q.n_lines + 63) / 64 < gdmk_mass3_seg_waves());
   double *tmp = nullptr;
   if (segmented) {
     if (op->mass_tmp_size < n) {  // once per operator (n is the owned size), freed with it

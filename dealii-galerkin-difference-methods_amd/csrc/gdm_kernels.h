@@ -139,6 +139,8 @@ hipError_t gdmk_launch_mass_lines(int p, int dir_kind, const double *src, double
 // mass inverse v3 single-sweep line solves (gdm_mass.hip); chunk length C(p)
 // (0 = unsupported degree); tables padded with zero rows to len + 3 C + p
 int gdmk_mass3_chunk(int p);
+// passes with fewer waves of lines than this run segmented (gdm_mass.hip)
+int gdmk_mass3_seg_waves();
 // allow_segments (src != dst only): lines of a pass with fewer than 512
 // waves are split into segments of >= 1 chunk with warm-ups (one more grid
 // dimension), so small meshes fill the GPU

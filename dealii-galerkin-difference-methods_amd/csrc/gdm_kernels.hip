@@ -31,7 +31,7 @@
 #define GDM_NP5 8
 #endif
 #ifndef GDM_PF5
-#define GDM_PF5 2
+#define GDM_PF5 3
 #endif
 #ifndef GDM_R7
 #define GDM_R7 2
@@ -50,21 +50,6 @@
 #endif
 #ifndef GDM_STENCIL_ST_NT
 #define GDM_STENCIL_ST_NT 1
-#endif
-#ifndef GDM_EXP_BSTORE
-#define GDM_EXP_BSTORE 1
-#endif
-#ifndef GDM_EXP_MULFIRST
-#define GDM_EXP_MULFIRST 1
-#endif
-#ifndef GDM_EXP_SXFOLD
-#define GDM_EXP_SXFOLD 1
-#endif
-#ifndef GDM_EXP_SLEEP
-#define GDM_EXP_SLEEP 1
-#endif
-#ifndef GDM_EXP_HALFG
-#define GDM_EXP_HALFG 1
 #endif
 #if GDM_STENCIL_ST_NT
 #define GDM_STENCIL_STORE(p, v) __builtin_nontemporal_store((v), (p))
@@ -174,6 +159,7 @@ struct Tile7 {
   int ry0;     // v8 y-wall tiles: first tile row of the column table (yb - y0)
   int lane, wv, x0, y0, zc0, zc1, zs, ze, zend;
   unsigned ooff;  // v8 consumers: byte offset of the lane's first output row in an output plane
+  int nyw;        // v8 y-wall tiles: producer waves that compute wall-row corrections
   // x wall columns inside this tile: nl from the left wall, nr from column rs on
   int nl, rs, ncw;
 };
@@ -897,11 +883,11 @@ __device__ __forceinline__ void sync_wait(lu32 *c, unsigned target) {
       "v_readfirstlane_b32 %1, %0\n\t"
       "s_cmp_ge_u32 %1, %3\n\t"
       "s_cbranch_scc1 2f\n\t"
-      "s_sleep %4\n\t"
+      "s_sleep 1\n\t"
       "s_branch 1b\n"
       "2:"
       : "=&v"(v), "=&s"(sv)
-      : "v"((unsigned)(uintptr_t)c), "s"(target), "n"(GDM_EXP_SLEEP)
+      : "v"((unsigned)(uintptr_t)c), "s"(target)
       : "memory", "scc");
 }
 
@@ -1005,39 +991,25 @@ __device__ __forceinline__ void xcalc8(const StencilArgs &a, const double (&w)[G
             V[j / 2].y = fma(IR::m[k], w[j + k + 1], V[j / 2].y);
         } else {
           V[j].x = fma(IR::m[k], w[j + k + 1], V[j].x);
-#if GDM_EXP_SXFOLD
           // B* = sx bhat * u with the scale folded into the run-time band
           // cxs = sx bhat (first half in SGPRs, hcoef), c[p] == 0 skipped
           if (BK != 1 || k != P) V[j].y = fma(hcoef<P, BK>(a.cxs, k), w[j + k + 1], V[j].y);
-#else
-          // the antisymmetric interior band has c[p] == 0: no FMA for it
-          if constexpr (BK == 1) {
-            if (IR::c[k] != 0.0) V[j].y = fma(IR::c[k], w[j + k + 1], V[j].y);
-          }
-          if constexpr (BK == 2) V[j].y = fma(IR::l[k], w[j + k + 1], V[j].y);
-#endif
         }
       }
   }
-#if !GDM_EXP_SXFOLD
-  if constexpr (BK != 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) V[j].y *= a.sx;
-  }
-#endif
 }
 
 // The last row group of a tile when it holds at most 2 rows (p = 5: rows
 // 40, 41 of 42): 2 rows x 64 x, two consecutive x per lane, so the wave
 // issues half the FMAs of a 4-row group (whose rows 42, 43 would be discarded)
 template <int P, int R, int NC, int NP, int BK>
-__device__ __forceinline__ void xsweep8_half(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g) {
+__device__ __forceinline__ void xload8_half(const Tile7 &t, lcdouble *us, int g,
+                                            double (&w)[Geom8<P, R, NC, NP, BK>::NWIN]) {
   using G = Geom8<P, R, NC, NP, BK>;
-  using IR = InteriorRows<P>;
-  constexpr int W = G::W, RL = G::RL, NW2 = 2 * P + 4;
+  constexpr int RL = G::RL, NW2 = 2 * P + 4;
+  static_assert(NW2 <= G::NWIN, "half window");
   const int rr = t.lane >> 5, q = t.lane & 31;
   const int r = 4 * g + rr;
-  double w[NW2];
   lcdouble2 *wp = (lcdouble2 *)(us + r * RL + 2 * q);
 #pragma unroll
   for (int i = 0; i < NW2 / 2; ++i) {
@@ -1045,6 +1017,16 @@ __device__ __forceinline__ void xsweep8_half(const StencilArgs &a, const Tile7 &
     w[2 * i] = v.x;
     w[2 * i + 1] = v.y;
   }
+}
+
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void xcalc8_half(const StencilArgs &a, const Tile7 &t, int g,
+                                            const double (&w)[Geom8<P, R, NC, NP, BK>::NWIN]) {
+  using G = Geom8<P, R, NC, NP, BK>;
+  using IR = InteriorRows<P>;
+  constexpr int W = G::W;
+  const int rr = t.lane >> 5, q = t.lane & 31;
+  const int r = 4 * g + rr;
   dpair V[2] = {dpair{0.0, 0.0}, dpair{0.0, 0.0}};
 #pragma unroll
   for (int k = 0; k < W; ++k)
@@ -1057,22 +1039,9 @@ __device__ __forceinline__ void xsweep8_half(const StencilArgs &a, const Tile7 &
           V[0].y = fma(IR::m[k], w[j + k + 1], V[0].y);
       } else {
         V[j].x = fma(IR::m[k], w[j + k + 1], V[j].x);
-#if GDM_EXP_SXFOLD
         if (BK != 1 || k != P) V[j].y = fma(hcoef<P, BK>(a.cxs, k), w[j + k + 1], V[j].y);
-#else
-        if constexpr (BK == 1) {
-          if (IR::c[k] != 0.0) V[j].y = fma(IR::c[k], w[j + k + 1], V[j].y);
-        }
-        if constexpr (BK == 2) V[j].y = fma(IR::l[k], w[j + k + 1], V[j].y);
-#endif
       }
     }
-#if !GDM_EXP_SXFOLD
-  if constexpr (BK != 0) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) V[j].y *= a.sx;
-  }
-#endif
   if (r < G::UR) {
     if constexpr (BK != 0) {
       ldouble2 *row = (ldouble2 *)(t.ab0 + r * G::ABRS);
@@ -1082,6 +1051,13 @@ __device__ __forceinline__ void xsweep8_half(const StencilArgs &a, const Tile7 &
       *(ldouble2 *)(t.ab0 + r * G::TX + 2 * q) = V[0];
     }
   }
+}
+
+template <int P, int R, int NC, int NP, int BK>
+__device__ __forceinline__ void xsweep8_half(const StencilArgs &a, const Tile7 &t, lcdouble *us, int g) {
+  double w[Geom8<P, R, NC, NP, BK>::NWIN];
+  xload8_half<P, R, NC, NP, BK>(t, us, g, w);
+  xcalc8_half<P, R, NC, NP, BK>(a, t, g, w);
 }
 
 template <int P, int R, int NC, int NP, int BK>
@@ -1260,15 +1236,29 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
     tt.ab0 = t.ab0 + slot * G::ABSZ;
     tt.yw = t.yw + (G::NYW == 2 ? slot : 0) * G::YWSZ;
     sync_wait(t.sync + SY_FREE + slot, NC * (i >> 1));
+    constexpr bool half_last = G::UR - 4 * (G::NG - 1) <= 2;
+    // the window reads of all this wave's row groups first: the second
+    // group's LDS latency overlaps the first group's FMAs (the compiler cannot
+    // hoist them itself past the (A, B) stores, which it cannot prove disjoint)
+    double win[G::NPASS][G::NWIN];
 #pragma unroll
     for (int ps = 0; ps < G::NPASS; ++ps) {
       const int g = t.wv + ps * NP;
       if (g < G::NG) {
-        constexpr bool half_last = GDM_EXP_HALFG && (G::UR - 4 * (G::NG - 1) <= 2);
+        if (half_last && g == G::NG - 1)
+          xload8_half<P, R, NC, NP, BK>(tt, u[slot], g, win[ps]);
+        else
+          xload8<P, R, NC, NP, BK>(tt, u[slot], g, win[ps]);
+      }
+    }
+#pragma unroll
+    for (int ps = 0; ps < G::NPASS; ++ps) {
+      const int g = t.wv + ps * NP;
+      if (g < G::NG) {
         if (half_last && g == G::NG - 1) {
-          xsweep8_half<P, R, NC, NP, BK>(a, tt, u[slot], g);
+          xcalc8_half<P, R, NC, NP, BK>(a, tt, g, win[ps]);
         } else {
-          xsweep8<P, R, NC, NP, BK>(a, tt, u[slot], g, V1);
+          xcalc8<P, R, NC, NP, BK>(a, win[ps], V1);
           write_ab8<P, R, NC, NP, BK>(tt, g, V1);
         }
         if (t.ncw > 0) {
@@ -1282,7 +1272,11 @@ __device__ __forceinline__ void producer8(const StencilArgs &a, const Tile7 &t) 
     // before the DMA that overwrites it)
     sync_signal(t.sync + SY_FULL + slot);
     if (i + 2 < n) stage_plane_pre7<P, R, NC, NP, BK, CH>(a, t, t.zs + i + 2, u[slot], dpre);
-    if (t.yedge) {
+    // y-wall tiles: only the waves that own a wall row (rows go to the waves
+    // from the last one down) wait for the whole plane and count in YWF; the
+    // others -- the first waves, which carry the second row groups -- go on
+    // to their next plane
+    if (t.yedge && NP - 1 - t.wv < t.nyw) {
       sync_wait(t.sync + SY_FULL + slot, NP * ((i >> 1) + 1));
       if constexpr (G::NYW == 1) sync_wait(t.sync + SY_YWR, NC * i);
       ywall8<P, R, NC, NP, BK>(a, tt);
@@ -1359,7 +1353,7 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
     ysweep8<P, R, NC, NP, BK, PF>(a, tt, D, E);
     if constexpr (YW) {
       if (ywave) {
-        sync_wait(t.sync + SY_YWF, NP * (i + 1));
+        sync_wait(t.sync + SY_YWF, t.nyw * (i + 1));
         const ldouble *yw = t.yw + (G::NYW == 2 ? bs : 0) * G::YWSZ;
         const int yb = ywall_begin<P, G::TY>(a, t.y0), ye = ywall_end<P, G::TY>(a, t.y0);
 #pragma unroll
@@ -1383,7 +1377,7 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
     // plane; its first term overwrites it (a multiply instead of a zeroing
     // move + FMA).  Outputs whose first plane zz + p - 2p precedes the chunk
     // start keep the ring's initial zeros and only ever see FMAs.
-    constexpr bool MF = GDM_EXP_MULFIRST;
+    constexpr bool MF = true;
     if constexpr (!WALL) {
       // interior z column: out += mhat[k] E + zd[k] D with zd = dint dhat[2p - k]
       // (the scale folded into the coefficients; zd[p] = 0 for advection)
@@ -1438,7 +1432,6 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
   const int zo = zz - P;
   if (zo >= t.zc0 && zo < t.zc1) {
     const int Nx = a.Nx, x = t.x0 + t.lane;
-#if GDM_EXP_BSTORE
     // buffer stores: the plane's base in the resource (scalar), the lane's
     // row offset a per-wave constant, row j's offset in soffset -- no 64-bit
     // per-lane address arithmetic per plane (non-temporal, cpol 2 = nt);
@@ -1449,25 +1442,8 @@ __device__ __forceinline__ void cplane8(const StencilArgs &a, const Tile7 &t, in
     for (int j = 0; j < R; ++j)
       if (full || (ybase + j < a.out_y1 && x < Nx))
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, acc[rslot][j]), rs, t.ooff, j * Nx * 8, 2);
-#else
-    {
-      double *orow = a.dst + ((int64_t)(zo - a.out_z0) * (a.out_y1 - a.out_y0) + (ybase - a.out_y0)) * Nx + x;
-      if (full) {
-#pragma unroll
-        for (int j = 0; j < R; ++j) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < R; ++j)
-          if (x < Nx && ybase + j < a.out_y1) GDM_STENCIL_STORE(orow + (int64_t)j * Nx, acc[rslot][j]);
-      }
-    }
-#endif
   }
-  if constexpr (!GDM_EXP_MULFIRST) {
-#pragma unroll
-    for (int j = 0; j < R; ++j) acc[rslot][j] = 0.0;
   }
-}
 
 template <int JP, int P, int R, int NC, int NP, int BK, int PF, bool WALL, bool YW>
 __device__ __forceinline__ void cblock8(const StencilArgs &a, const Tile7 &t, int ybase, bool full, bool ywave,
@@ -1604,6 +1580,7 @@ __global__ void __launch_bounds__(64 * (NP + NC), ((NP + NC) * Geom8<P, R, NC, N
   const int yb = ywall_begin<P, G::TY>(a, t.y0);
   t.yedge = yb >= 0;
   t.ry0 = yb - t.y0;
+  t.nyw = t.yedge ? min(NP, ywall_end<P, G::TY>(a, t.y0) - yb) : 0;
   {
     const int r = bz < a.nchunk0 ? 0 : 1;
     const int c = bz - (r ? a.nchunk0 : 0);

@@ -314,6 +314,11 @@ struct Geo3 {
 // table / interior-row decision measured slower: SGPR spills, round 2)
 #define GDM_MASS_EDGE_MODE 1
 
+// passes with fewer waves of lines than this split their lines into segments
+#ifndef GDM_MASS_SEG_WAVES
+#define GDM_MASS_SEG_WAVES 512
+#endif
+
 // compiler-only fence: the scheduler may not move instructions across it
 #define GDM_FENCE()                    \
   do {                                 \
@@ -836,7 +841,7 @@ hipError_t launch_mass3_p(int dir_kind, const double *src, double *dst, int len,
   constexpr int C = Geo3<P>::C;
   const int n_chunks = (len + C - 1) / C;
   int seg_chunks = 0, n_segs = 1;
-  if (allow_segments && src != dst && grid < 512 && n_chunks >= 4) {
+  if (allow_segments && src != dst && grid < GDM_MASS_SEG_WAVES && n_chunks >= 4) {
     const int want = (int)std::min<int64_t>(n_chunks, (1024 + grid - 1) / grid);
     seg_chunks = (n_chunks + want - 1) / want;
     n_segs = (n_chunks + seg_chunks - 1) / seg_chunks;
@@ -911,6 +916,8 @@ extern "C" hipError_t gdmk_launch_mass3_rk(int p, const double *src, int len, in
 // row (l[p], u[p], d) that rows [row_lo, row_hi) (urow: [row_lo, row_hi - p))
 // hold exactly.
 // dir_kind 0 (contiguous lines) requires len even and 16-B aligned src / dst.
+extern "C" int gdmk_mass3_seg_waves() { return GDM_MASS_SEG_WAVES; }
+
 extern "C" int gdmk_mass3_chunk(int p) {
   switch (p) {
     case 3: return gdmk::Geo3<3>::C;
