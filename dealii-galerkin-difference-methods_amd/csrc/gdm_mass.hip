@@ -314,9 +314,13 @@ struct Geo3 {
 // table / interior-row decision measured slower: SGPR spills, round 2)
 #define GDM_MASS_EDGE_MODE 1
 
-// passes with fewer waves of lines than this split their lines into segments
+// passes with fewer waves of lines than this split their lines into segments:
+// one wave per SIMD (1024 on the chip) is these kernels' occupancy.  512 ->
+// 1024 moved the C3 rank's (512^2 x 64 planes) y and x passes, 512 waves each,
+// to two segments: SPIKE solve 0.335 / 0.340 -> 0.304 / 0.314 ms (same box,
+// gpurun_out r6f rank legs)
 #ifndef GDM_MASS_SEG_WAVES
-#define GDM_MASS_SEG_WAVES 512
+#define GDM_MASS_SEG_WAVES 1024
 #endif
 
 // compiler-only fence: the scheduler may not move instructions across it
