@@ -1964,16 +1964,12 @@ template <int P, int R, int NC, int NP, int PF>
 static hipError_t launch8_p(int bk, const StencilArgs &a, const TailReq &tail, hipStream_t st) {
   const bool vec = (a.Nx % 2 == 0) && ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0);
   switch (bk) {
-#ifdef GDM_ONLY_ADV16  // fast experiment builds: advection, 16-B DMA only
-    case 1: return vec ? launch8_t<P, R, NC, NP, 1, 16, PF>(a, tail, st) : hipErrorInvalidValue;
-#else
     case 0:
       return vec ? launch8_t<P, R, NC, NP, 0, 16, PF>(a, tail, st) : launch8_t<P, R, NC, NP, 0, 4, PF>(a, tail, st);
     case 1:
       return vec ? launch8_t<P, R, NC, NP, 1, 16, PF>(a, tail, st) : launch8_t<P, R, NC, NP, 1, 4, PF>(a, tail, st);
     case 2:
       return vec ? launch8_t<P, R, NC, NP, 2, 16, PF>(a, tail, st) : launch8_t<P, R, NC, NP, 2, 4, PF>(a, tail, st);
-#endif
     default: return hipErrorInvalidValue;
   }
 }

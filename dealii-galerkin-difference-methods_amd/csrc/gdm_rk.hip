@@ -211,24 +211,38 @@ __global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps,
       }
     }
     if (mode == 1) {
+      // every load of the line's edge planes first, then the stores: one
+      // memory latency per line instead of one per plane (the compiler keeps
+      // loads behind stores to the same array)
+      double gf[P], gl[P];
 #pragma unroll
       for (int a = 0; a < P; ++a) {
-        double gf = xo[(int64_t)a * ps], gl = xo[(int64_t)(n - P + a) * ps];
         if (round == 0) {
-          G0[(int64_t)a * ps + i] = gf;
-          G0[(int64_t)(P + a) * ps + i] = gl;
+          gf[a] = xo[(int64_t)a * ps];
+          gl[a] = xo[(int64_t)(n - P + a) * ps];
         } else {
-          gf = G0[(int64_t)a * ps + i];
-          gl = G0[(int64_t)(P + a) * ps + i];
+          gf[a] = G0[(int64_t)a * ps + i];
+          gl[a] = G0[(int64_t)(P + a) * ps + i];
         }
+      }
+      if (round == 0) {
+#pragma unroll
+        for (int a = 0; a < P; ++a) {
+          G0[(int64_t)a * ps + i] = gf[a];
+          G0[(int64_t)(P + a) * ps + i] = gl[a];
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < P; ++a) {
         const double *vf = VW + (size_t)a * 2 * P, *wl = VW + (size_t)(n - P + a) * 2 * P + P;
+        double f = gf[a], l = gl[a];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-          gf = fma(-vf[j], t[j], gf);
-          gl = fma(-wl[j], b[j], gl);
+          f = fma(-vf[j], t[j], f);
+          l = fma(-wl[j], b[j], l);
         }
-        xo[(int64_t)a * ps] = gf;
-        xo[(int64_t)(n - P + a) * ps] = gl;
+        xo[(int64_t)a * ps] = f;
+        xo[(int64_t)(n - P + a) * ps] = l;
       }
       continue;
     }
@@ -246,14 +260,26 @@ __global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps,
         if (has_hi) xo[(int64_t)(n + a) * ps] = t[a];
       }
     }
-    for (int k = k_begin; k < k_end; ++k) {
-      const double *vw = VW + (size_t)k * 2 * P;
-      double c = 0.0;
+    // the correction in blocks of KB planes: the block's loads are issued
+    // together (one memory latency per block, not per plane)
+    constexpr int KB = 8;
+    for (int k0 = k_begin; k0 < k_end; k0 += KB) {
+      double xv[KB];
 #pragma unroll
-      for (int j = 0; j < P; ++j) c = fma(vw[j], t[j], c);
+      for (int u = 0; u < KB; ++u)
+        if (k0 + u < k_end) xv[u] = xo[(int64_t)(k0 + u) * ps];
 #pragma unroll
-      for (int j = 0; j < P; ++j) c = fma(vw[P + j], b[j], c);
-      xo[(int64_t)k * ps] -= c;
+      for (int u = 0; u < KB; ++u) {
+        if (k0 + u < k_end) {
+          const double *vw = VW + (size_t)(k0 + u) * 2 * P;
+          double c = 0.0;
+#pragma unroll
+          for (int j = 0; j < P; ++j) c = fma(vw[j], t[j], c);
+#pragma unroll
+          for (int j = 0; j < P; ++j) c = fma(vw[P + j], b[j], c);
+          xo[(int64_t)(k0 + u) * ps] = xv[u] - c;
+        }
+      }
     }
   }
 }

@@ -2,7 +2,7 @@
 # Experiment build for an on-box A/B of the stencil:
 #   tools/build_variant.sh NAME [hipcc -D flags...]  -> dealii-galerkin-difference-methods_amd/lib/ab/NAME/libgdm_hip.so
 # gdm_kernels.hip is rebuilt with the flags (ONLY_P=5 by default: that degree's
-# stencil only; ONLY_ADV16=1: advection with 16-B DMA only; BUILD_CAPI=1: gdm_capi.cpp
+# stencil only; BUILD_CAPI=1: gdm_capi.cpp
 # too; BUILD_MASS=1: gdm_mass.hip too; BUILD_KERNELS=0: the in-tree stencil object),
 # every other object comes from the in-tree build (lib/obj).  Select it
 # with GDM_HIP_LIB (tools/gpu_ab.sh, tools/time_apply.py) and delete
@@ -13,7 +13,6 @@ B=/root/repo/dealii-galerkin-difference-methods_amd/lib/obj
 O=/root/repo/dealii-galerkin-difference-methods_amd/lib/ab/$NAME
 mkdir -p $O
 X=""
-[ "${ONLY_ADV16:-0}" = 1 ] && X="-DGDM_ONLY_ADV16"
 F="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -Wno-unused-function -DGDM_ONLY_P=${ONLY_P:-5} $X $*"
 CAPI=$B/gdm_capi.o
 if [ "${BUILD_CAPI:-0}" = 1 ]; then
