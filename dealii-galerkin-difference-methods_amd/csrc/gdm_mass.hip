@@ -627,8 +627,10 @@ __global__ void __launch_bounds__(64) mass3_strided_kernel(const double *src, do
 // Requires len even and 16-B aligned src / dst (host-checked).
 // RKM (the RK stage update fused into the store, gdmk_launch_mass3_rk): 0 = store
 // the solution into dst; 1 = acc_out = acc_in + beta k; 2 = also Y = y + alpha
-// k.  acc_in / y of the chunk to be stored are loaded into registers before the
-// chunk's arithmetic (their latency hides behind it); k never reaches memory.
+// k; 3 = 2 with acc_in == y (the first RK stage: one load serves both, 8 B per
+// DoF less).  acc_in / y of the chunk to be stored are loaded into registers
+// before the chunk's arithmetic (their latency hides behind it); k never
+// reaches memory.
 template <int P, bool SEG, int RKM = 0>
 __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, double *dst, int len, int64_t n_lines,
                                                         const double *__restrict__ lrow,
@@ -640,7 +642,7 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
   constexpr int C = R::C, UPR = G::UPR, QL = G::QL;
   static_assert(RKM == 0 || !SEG, "the fused RK update runs unsegmented");
   // stores in flight after the last load of an iteration (the loop-top wait)
-  constexpr int NST = UPR * (RKM == 2 ? 2 : 1);
+  constexpr int NST = UPR * (RKM >= 2 ? 2 : 1);
   extern __shared__ __attribute__((aligned(16))) char smem3[];
   ldouble2 *tile0 = (ldouble2 *)smem3;
   ldouble2 *tile1 = tile0 + G::TILE;
@@ -691,7 +693,7 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
   };
   // the RK operands of the chunk at `base` (RKM > 0), fetched one chunk of
   // arithmetic ahead of their use
-  dpair pa[RKM ? UPR : 1], py[RKM == 2 ? UPR : 1];
+  dpair pa[RKM ? UPR : 1], py[RKM >= 2 ? UPR : 1];
   const int64_t obase = l0 * len;
   auto prefetch = [&](int base) {
     if constexpr (RKM > 0) {
@@ -705,6 +707,7 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
         const int64_t e = obase + (int64_t)row * len + base + 2 * pair;
         pa[q] = __builtin_nontemporal_load(reinterpret_cast<const dpair *>(rk.acc_in + e));
         if constexpr (RKM == 2) py[q] = __builtin_nontemporal_load(reinterpret_cast<const dpair *>(rk.y + e));
+        if constexpr (RKM == 3) py[q] = pa[q];
       }
     }
   };
@@ -724,7 +727,7 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
         const dpair bv = {rk.beta, rk.beta};
         __builtin_nontemporal_store(__builtin_elementwise_fma(bv, v, pa[q]),
                                     reinterpret_cast<dpair *>(rk.acc_out + e));
-        if constexpr (RKM == 2) {
+        if constexpr (RKM >= 2) {
           const dpair av = {rk.alpha, rk.alpha};
           __builtin_nontemporal_store(__builtin_elementwise_fma(av, v, py[q]), reinterpret_cast<dpair *>(rk.Y + e));
         }
@@ -886,7 +889,10 @@ hipError_t launch_mass3_rk_p(const double *src, int len, int64_t n_lines, const 
   k.row_hi = row_hi;
   const unsigned grid = (unsigned)((n_lines + 63) / 64);
   constexpr size_t lds = Geo3<P>::lds_bytes();
-  if (rk.Y)
+  if (rk.Y && rk.acc_in == rk.y)
+    hipLaunchKernelGGL((mass3_rows_kernel<P, false, 3>), dim3(grid), dim3(64), lds, st, src, nullptr, len, n_lines,
+                       lrow, urow, invd, k, 0, rk);
+  else if (rk.Y)
     hipLaunchKernelGGL((mass3_rows_kernel<P, false, 2>), dim3(grid), dim3(64), lds, st, src, nullptr, len, n_lines,
                        lrow, urow, invd, k, 0, rk);
   else

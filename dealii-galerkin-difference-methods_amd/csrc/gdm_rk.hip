@@ -38,10 +38,11 @@ namespace gdmk {
 // 4096-block grid-stride loop (tools/rk_bench.hip, profiles/r3u).  The odd
 // tail element, if any, is done by the first lane.  Host-checked: every
 // pointer 16-B aligned.
-template <bool WITH_Y>
+// AY: acc_in == y (the first RK stage): one load serves both (8 B per entry less)
+template <bool WITH_Y, bool AY = false>
 __global__ void __launch_bounds__(256) rk_update2_kernel(int64_t n, double beta, const double *__restrict__ k,
                                                          const double *acc_in, double *acc_out, double alpha,
-                                                         const double *__restrict__ y, double *__restrict__ Y) {
+                                                         const double *y, double *__restrict__ Y) {
   using d2 = double __attribute__((ext_vector_type(2)));
   const int64_t n2 = n / 2, stride = (int64_t)gridDim.x * blockDim.x;
   const d2 *k2 = reinterpret_cast<const d2 *>(k), *a2 = reinterpret_cast<const d2 *>(acc_in);
@@ -52,7 +53,7 @@ __global__ void __launch_bounds__(256) rk_update2_kernel(int64_t n, double beta,
     const d2 ai = __builtin_nontemporal_load(a2 + i);
     // one FMA per update (the arithmetic of the x pass with the update fused, gdm_mass.hip)
     if (WITH_Y) {
-      const d2 yi = __builtin_nontemporal_load(reinterpret_cast<const d2 *>(y) + i);
+      const d2 yi = AY ? ai : __builtin_nontemporal_load(reinterpret_cast<const d2 *>(y) + i);
       __builtin_nontemporal_store(__builtin_elementwise_fma(av, ki, yi), reinterpret_cast<d2 *>(Y) + i);
     }
     __builtin_nontemporal_store(__builtin_elementwise_fma(bv, ki, ai), o2 + i);
@@ -320,7 +321,10 @@ extern "C" hipError_t gdmk_launch_rk_update(int64_t n, double beta, const double
   auto al16 = [](const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (al16(k) && al16(acc_in) && al16(acc_out) && (!Y || (al16(y) && al16(Y)))) {
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n / 2 + 255) / 256, (int64_t)1 << 30));
-    if (Y)
+    if (Y && y == acc_in)
+      hipLaunchKernelGGL((gdmk::rk_update2_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, st, n, beta, k,
+                         acc_in, acc_out, alpha, y, Y);
+    else if (Y)
       hipLaunchKernelGGL(gdmk::rk_update2_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, n, beta, k, acc_in,
                          acc_out, alpha, y, Y);
     else
