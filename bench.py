@@ -376,6 +376,30 @@ def c3_rank_slab(steps=10, n_ranks=8, rank=3):
         op.mass_solve_interface_ghosts(x)
 
     spike = timed(solve)
+    # the whole one-exchange RK stage of this rank without its exchanges
+    # (SlabRK4 / the C++ one_exchange_per_stage): compute_rhs into k's owned
+    # planes, the slab solve in place, the refinement rounds, then the
+    # interface correction fused with the stage update over the local vectors
+    # (gdm_mass_solve_interface_rk) -- or, unfused, interface_ghosts +
+    # rk_update over n_local (the same bits)
+    k = op.new_vector(True)
+    acc, Y = op.new_vector(True), op.new_vector(True)
+    kown = op.owned_view(k)
+
+    def stage(fused):
+        op.apply(u, kown, bc if op.n_bc_points else None)
+        op.mass_solve_slab(kown, kown)
+        for q in range(rounds):
+            op.mass_solve_interface_round(k, q)
+        if fused:
+            op.mass_solve_interface_rk(k, 0.1, acc, acc, 0.05, u, Y)
+        else:
+            op.mass_solve_interface_ghosts(k)
+            op.rk_update(0.1, k, acc, acc, 0.05, u, Y)
+
+    stage_fused = timed(lambda: stage(True))
+    stage_unfused = timed(lambda: stage(False))
+    del k, acc, Y, kown
     N = op.n_owned
     n_int = (hi - lo) * L["plane_size"]
     res = {
@@ -392,6 +416,8 @@ def c3_rank_slab(steps=10, n_ranks=8, rank=3):
         "spike_solve_ms": spike,
         "spike_rounds": rounds,
         "mass_solve_frac": BYTES_PER_DOF * N / (spike * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "rk_stage_ms": stage_fused,
+        "rk_stage_unfused_ms": stage_unfused,
     }
     del op, u, v, x, r, bc
     torch.cuda.empty_cache()

@@ -1664,6 +1664,43 @@ int gdm_mass_solve_interface(gdm_op *op, double *x_local) { return mass_solve_in
 
 int gdm_mass_solve_interface_ghosts(gdm_op *op, double *x_local) { return mass_solve_interface_impl(op, x_local, true); }
 
+int gdm_mass_solve_interface_rk(gdm_op *op, const double *x_local, double beta, const double *acc_in, double *acc_out,
+                                double alpha, const double *y, double *Y) {
+  if (!op) return fail(GDM_ERR_ARG, "op is NULL");
+  if (op->mesh.n_ranks == 1)
+    return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_interface_rk: multi-rank only (one rank: gdm_mass_apply_inverse_rk)");
+  if (!op->spike.built || op->spike.rounds < 0 || op->spike.next_round < 0)
+    return fail(GDM_ERR_STATE, "gdm_mass_solve_interface_rk: call gdm_mass_solve_slab first");
+  if (op->spike.next_round != op->spike.rounds)
+    return fail(GDM_ERR_STATE, "gdm_mass_solve_interface_rk: not every refinement round ran since gdm_mass_solve_slab");
+  if (op->layout.n_owned > 0 && (!x_local || !acc_in || !acc_out || (Y && !y)))
+    return fail(GDM_ERR_ARG, "NULL vector");
+  {
+    const int64_t n = op->layout.n_local;
+    auto overlap = [n](const void *a, const void *b) {
+      const double *p = (const double *)a, *q = (const double *)b;
+      return p && q && p < q + n && q < p + n;
+    };
+    if (overlap(x_local, acc_out) || overlap(x_local, Y) || (Y && overlap(acc_out, Y)) ||
+        (Y && overlap(Y, acc_in)) || (Y && overlap(Y, y) && Y != y) || (overlap(acc_out, y) && acc_out != y) ||
+        (overlap(acc_out, acc_in) && acc_out != acc_in))
+      return fail(GDM_ERR_ARG, "gdm_mass_solve_interface_rk: x_local must not overlap the outputs; acc_out / Y may "
+                               "only equal (not partially overlap) an input");
+  }
+  GDM_GUARD_BEGIN
+  hip_check(hipSetDevice(op->device), "hipSetDevice");
+  op->spike.next_round = -1;
+  const SpikeTables &S = op->spike;
+  const gdm_layout &L = op->layout;
+  const gdmk::RkOut rk{acc_in, acc_out, y, Y, beta, alpha};
+  hip_check(gdmk_launch_spike_rk(op->p, x_local, L.plane_size, L.ghost_planes_below, L.ghost_planes_above,
+                                 S.n_planes, S.has_lo, S.has_hi, S.VW, S.S, S.k_begin, S.k_end,
+                                 S.rounds > 0 ? S.G0 : nullptr, rk, op->stream),
+            "spike_rk");
+  return GDM_OK;
+  GDM_GUARD_END
+}
+
 static int mass_solve_interface_impl(gdm_op *op, double *x_local, bool ghosts) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   if (op->mesh.n_ranks == 1) return GDM_OK;

@@ -70,6 +70,10 @@ struct BcStage {
 
 }  // namespace gdmk
 
+namespace gdmk {
+struct RkOut;  // gdm_kernels.h
+}
+
 extern "C" {
 // gdm_rk.hip: acc_out = acc_in + beta k; Y = y + alpha k (Y may be NULL)
 hipError_t gdmk_launch_rk_update(int64_t n, double beta, const double *k, const double *acc_in, double *acc_out,
@@ -85,6 +89,12 @@ hipError_t gdmk_launch_periodic(double *v, const int64_t N[3], int d, int mode, 
 // the owned first / last p planes become g_first - V[0:p] t / g_last - W[n-p:n] b
 // with g saved to G0 [2p][plane_size] at round 0.  mode 2: mode 0, and b / t
 // overwrite the ghost planes below / above (the neighbours' edge planes of x)
+// the interface correction fused with the one-exchange RK stage update
+// (gdm_mass_solve_interface_rk): k of every local plane -> acc_out = acc_in +
+// beta k, Y = y + alpha k (rk.Y may be NULL); x_local is only read
+hipError_t gdmk_launch_spike_rk(int p, const double *x_local, int64_t plane_size, int ghost_below, int ghost_above,
+                                int n_planes, int has_lo, int has_hi, const double *VW, const double *S, int k_begin,
+                                int k_end, const double *G0, const gdmk::RkOut &rk, hipStream_t st);
 hipError_t gdmk_launch_spike(int p, double *x_local, int64_t plane_size, int64_t own_off, int n_planes, int has_lo,
                              int has_hi, const double *VW, const double *S, int k_begin, int k_end, int mode,
                              int round, double *G0, hipStream_t st);

@@ -146,6 +146,7 @@ def load():
         "gdm_mass_solve_slab": [P, P, P],
         "gdm_mass_solve_interface": [P, P],
         "gdm_mass_solve_interface_ghosts": [P, P],
+        "gdm_mass_solve_interface_rk": [P, P, d, P, P, d, P, P],
         "gdm_mass_solve_interface_round": [P, P, i32],
         "gdm_mass_spike_rounds": [P, ctypes.POINTER(ctypes.c_int)],
         "gdm_synchronize": [P],

@@ -274,19 +274,23 @@ class SlabRK4:
     of thin slabs).  The ghost planes then carry the neighbours' values as the
     interface solution gives them (<= 1e-15 relative apart from the owner's,
     the truncation of the interface systems); `resync` > 0 exchanges y's ghost
-    planes every `resync` steps.
+    planes every `resync` steps.  fused (one_exchange only): the interface
+    correction and the stage update run as one launch
+    (gdm_mass_solve_interface_rk), k is never stored -- the same bits.
 
     The inflow data of a built-in boundary function (fn_kind, fn_params) are
     computed by the engine per stage (gdm_apply_bc_fn); fn_kind None: no inflow
     data.  State: self.y[r] (local vectors); the owned values are
     ops[r].owned_view(self.y[r])."""
 
-    def __init__(self, ops, exchange, fn_kind=None, fn_params=(), one_exchange=True, rounds=None, resync=0):
+    def __init__(self, ops, exchange, fn_kind=None, fn_params=(), one_exchange=True, rounds=None, resync=0,
+                 fused=True):
         from . import _capi
 
         self.ops, self.exchange = list(ops), exchange
         self.fn, self.prm = fn_kind, list(fn_params)
         self.one = bool(one_exchange)
+        self.fused = self.one and bool(fused)
         self.rounds = _capi.mesh_spike_rounds(self.ops[0].mesh) if rounds is None else int(rounds)
         if self.rounds < 0:
             raise ValueError("SlabRK4: the partition is too thin for the SPIKE mass inverse")
@@ -320,6 +324,8 @@ class SlabRK4:
             for op, k in zip(self.ops, self._k):
                 op.mass_solve_interface_round(k, rnd)
             self.exchange(self._k)
+        if self.fused:
+            return
         for op, k in zip(self.ops, self._k):
             if self.one:
                 op.mass_solve_interface_ghosts(k)
@@ -334,7 +340,11 @@ class SlabRK4:
             self._rhs(t, h, s, stage)
             last = s == 3
             for op, k, y, acc, Y in zip(self.ops, self._k, self.y, self._acc, self._Y):
-                if last:
+                if self.fused and last:
+                    op.mass_solve_interface_rk(k, h * RK4_B[s], acc, y)
+                elif self.fused:
+                    op.mass_solve_interface_rk(k, h * RK4_B[s], y if s == 0 else acc, acc, h * RK4_A[s], y, Y)
+                elif last:
                     op.rk_update(h * RK4_B[s], k, acc, y)
                 else:
                     op.rk_update(h * RK4_B[s], k, y if s == 0 else acc, acc, h * RK4_A[s], y, Y)

@@ -271,6 +271,21 @@ class GdmOperator:
         check(self.lib.gdm_mass_solve_interface_ghosts(self.h, _ptr(x_local)), "gdm_mass_solve_interface_ghosts")
         return x_local
 
+    def mass_solve_interface_rk(self, x_local, beta, acc_in, acc_out, alpha=0.0, y=None, Y=None):
+        """mass_solve_interface_ghosts fused with rk_update over the local
+        vectors (gdm_mass_solve_interface_rk): acc_out = acc_in + beta k, Y =
+        y + alpha k (when Y is given) with k the interface-corrected solve of
+        every local plane; x_local is only read.  The bits of
+        mass_solve_interface_ghosts(x) + rk_update(beta, x, ...)."""
+        n = self.n_local
+        for v in (x_local, acc_in, acc_out) + ((y, Y) if Y is not None else ()):
+            if v.numel() != n:
+                raise GdmError("mass_solve_interface_rk: vectors need n_local = %d entries" % n)
+        check(self.lib.gdm_mass_solve_interface_rk(self.h, _ptr(x_local), float(beta), _ptr(acc_in), _ptr(acc_out),
+                                                   float(alpha), _ptr(y) if Y is not None else None, _ptr(Y)),
+              "gdm_mass_solve_interface_rk")
+        return acc_out
+
     def error_norms(self, u_local, fn_kind, params, t, cell_errors=None):
         """(Linf, L1, L2) of u - f(t) over QGauss(p+1) on the owned cells
         (advection/problem.h:269-425 postprocess, volume part); cell_errors

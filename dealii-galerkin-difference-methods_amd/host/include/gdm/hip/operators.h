@@ -510,6 +510,13 @@ class MassMatrixOperator {
   // the interface systems (gdm_mass_solve_interface_ghosts): one exchange
   // (+ the refinement rounds of thin slabs), no copy
   void solve_spike_local(DeviceVector &x_local, Communicator &comm) const {
+    solve_spike_local_pending(x_local, comm);
+    check(gdm_mass_solve_interface_ghosts(op, x_local.get_values()), "gdm_mass_solve_interface_ghosts");
+  }
+  // solve_spike_local up to (not including) the interface correction: the
+  // slab solve, its exchange and the refinement rounds; finish with
+  // spike_stage_update (the correction fused with the RK stage update)
+  void solve_spike_local_pending(DeviceVector &x_local, Communicator &comm) const {
     if (x_local.size() != (std::size_t)layout.n_local) throw Error("solve_spike_local: x must be a local vector");
     if (sp_rounds < 0) sp_rounds = spike_rounds();
     double *own = x_local.get_values() + layout.ghost_planes_below * layout.plane_size;
@@ -519,7 +526,21 @@ class MassMatrixOperator {
       check(gdm_mass_solve_interface_round(op, x_local.get_values(), k), "gdm_mass_solve_interface_round");
       comm.update_ghost_values(op, x_local);
     }
-    check(gdm_mass_solve_interface_ghosts(op, x_local.get_values()), "gdm_mass_solve_interface_ghosts");
+  }
+  // rk4_stage_update of local vectors with k = the interface-corrected solve
+  // pending in x_local (gdm_mass_solve_interface_rk: one launch, k not stored;
+  // the bits of solve_spike_local + rk4_stage_update)
+  void spike_stage_update(int s, double h, const DeviceVector &x_local, DeviceVector &y, DeviceVector &acc,
+                          DeviceVector &Y) const {
+    if (s == 3)
+      check(gdm_mass_solve_interface_rk(op, x_local.get_values(), h * ClassicRK4::b[3], acc.get_values(),
+                                        y.get_values(), 0.0, nullptr, nullptr),
+            "gdm_mass_solve_interface_rk");
+    else
+      check(gdm_mass_solve_interface_rk(op, x_local.get_values(), h * ClassicRK4::b[s],
+                                        (s == 0 ? y : acc).get_values(), acc.get_values(), h * ClassicRK4::a[s + 1],
+                                        y.get_values(), Y.get_values()),
+            "gdm_mass_solve_interface_rk");
   }
   gdm_op *handle() const { return op; }
 
@@ -606,7 +627,8 @@ class AdvectionProblem {
           stiffness_matrix_operator.compute_rhs_fn(result.block(1), y.block(1), t0, bc_alpha, bc_tk);
         else
           stiffness_matrix_operator.compute_rhs(result, y, time);
-        mass_matrix_operator.solve_spike_local(result.block(1), *comm);
+        // the interface correction runs fused with the stage update below
+        mass_matrix_operator.solve_spike_local_pending(result.block(1), *comm);
         return;
       }
       if (in_faces) {
@@ -647,7 +669,11 @@ class AdvectionProblem {
         bc_tk = s == 0 ? t0 : t0 + ClassicRK4::c[s - 1] * h;
         fu_rhs(t0 + ClassicRK4::c[s] * h, s == 0 ? solution : stage, k);  // ghosts of the stage exchanged
         for (unsigned int bl = in_faces ? 1 : 0; bl < 2; ++bl)
-          rk4_stage_update(s, h, k.block(bl), solution.block(bl), acc.block(bl), stage.block(bl));
+          if (one_exchange && bl == 1)
+            mass_matrix_operator.spike_stage_update(s, h, k.block(1), solution.block(1), acc.block(1),
+                                                    stage.block(1));
+          else
+            rk4_stage_update(s, h, k.block(bl), solution.block(bl), acc.block(bl), stage.block(bl));
       }
       time.advance_time();
       ++n;

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GDM_HIP_ABI_VERSION 14
+#define GDM_HIP_ABI_VERSION 15
 
 enum gdm_status {
   GDM_OK = 0,
@@ -255,6 +255,18 @@ int gdm_mass_solve_interface(gdm_op *op, double *x_local);
  * needs no update_ghost_values before the next stage's stencil
  * (advection/stiffness.h:343) -- one exchange per stage, the SPIKE one. */
 int gdm_mass_solve_interface_ghosts(gdm_op *op, double *x_local);
+/* The interface step of the one-exchange stage fused with its RK update
+ * (ABI 15): k = M^-1 rhs on every plane of the local layout (the owned planes
+ * corrected as gdm_mass_solve_interface does, the ghost planes the interface
+ * solution as gdm_mass_solve_interface_ghosts writes them) goes straight into
+ * acc_out = acc_in + beta k and, when Y != NULL, Y = y + alpha k -- local
+ * vectors (n_local entries), the arithmetic and the bits of
+ * gdm_mass_solve_interface_ghosts + gdm_vec_rk_update over n_local; k is not
+ * stored (x_local, holding the slab solve and the exchanged planes, is only
+ * read).  acc_out may equal acc_in (not partially overlap it), y may equal
+ * acc_in; x_local must not overlap an output.  Multi-rank only. */
+int gdm_mass_solve_interface_rk(gdm_op *op, const double *x_local, double beta, const double *acc_in, double *acc_out,
+                                double alpha, const double *y, double *Y);
 
 /* x_owned = M^-1 rhs_owned by SolverCG on the matrix-free mass operator with
  * ReductionControl(max_it, abs_tol, rel_tol) semantics, the solve of

@@ -160,6 +160,92 @@ def test_interface_ghosts_give_the_neighbours_planes(dim, p, n, R):
         assert float((x - y).abs().max()) <= 1e-13 * scale
 
 
+@pytest.mark.parametrize("dim,p,n,R", [(3, 5, (12, 10, 130), 2), (2, 3, (20, 150), 3), (1, 5, 400, 4),
+                                       (3, 7, (8, 9, 255), 8), (3, 5, (33, 17, 200), 5)])
+def test_interface_rk_is_interface_ghosts_plus_update_bitwise(dim, p, n, R):
+    """gdm_mass_solve_interface_rk (ABI 15): the interface correction fused
+    with the stage update -- every local plane of acc_out / Y, ghost planes
+    included, has the bits of mass_solve_interface_ghosts + rk_update over
+    n_local, for the three argument patterns of the low-storage RK4 stages
+    (acc_in == y at stage 0, acc_in == acc_out in between, no Y at the last),
+    with and without refinement rounds (C4 at 8 ranks: one round)."""
+    import gdm_amd
+
+    rounds = gdm_amd._capi.mass_spike_rounds(dim, p, n, R)
+    assert rounds >= 0
+    one = gdm_amd.GdmOperator(dim, p, n, 0.0, 1.0, "mass")
+    r = torch.from_numpy(np.random.default_rng(9).uniform(-1, 1, one.n_owned)).cuda()
+    del one
+    ops = _ranks(gdm_amd, dim, p, n, R)
+    gen = torch.Generator(device="cuda").manual_seed(4)
+
+    def solved():
+        xs = []
+        for op in ops:
+            a = op.layout["owned_plane_begin"] * op.layout["plane_size"]
+            x = torch.rand(op.n_local, dtype=torch.float64, device="cuda", generator=gen)  # ghosts: stale data
+            op.mass_solve_slab(r[a:a + op.n_owned].contiguous(), op.owned_view(x))
+            xs.append(x)
+        torch.cuda.synchronize()
+        _exchange(ops, xs)
+        for k in range(rounds):
+            for op, x in zip(ops, xs):
+                op.mass_solve_interface_round(x, k)
+            torch.cuda.synchronize()
+            _exchange(ops, xs)
+        return xs
+
+    beta, alpha = 0.37, -1.25
+    for pattern in ("stage0", "middle", "last"):
+        ks = [op.mass_solve_interface_ghosts(x) for op, x in zip(ops, solved())]
+        xs_copy = solved()  # a second solve for the fused call (same bits)
+        for op, k, xc in zip(ops, ks, xs_copy):
+            y = torch.rand(op.n_local, dtype=torch.float64, device="cuda", generator=gen)
+            acc = torch.rand_like(y)
+            want_acc, want_Y = torch.empty_like(y), torch.empty_like(y)
+            got_acc, got_Y = torch.empty_like(y), torch.empty_like(y)
+            if pattern == "stage0":
+                op.rk_update(beta, k, y, want_acc, alpha, y, want_Y)
+                op.mass_solve_interface_rk(xc, beta, y, got_acc, alpha, y, got_Y)
+            elif pattern == "middle":
+                want_acc.copy_(acc)
+                got_acc.copy_(acc)
+                op.rk_update(beta, k, want_acc, want_acc, alpha, y, want_Y)
+                op.mass_solve_interface_rk(xc, beta, got_acc, got_acc, alpha, y, got_Y)
+            else:
+                op.rk_update(beta, k, acc, want_acc)
+                op.mass_solve_interface_rk(xc, beta, acc, got_acc)
+            torch.cuda.synchronize()
+            assert torch.equal(got_acc, want_acc), (pattern, float((got_acc - want_acc).abs().max()))
+            if pattern != "last":
+                assert torch.equal(got_Y, want_Y), pattern
+        # the fused call consumes the solve like the interface call
+        v0 = ops[0].new_vector(True)
+        with pytest.raises(gdm_amd.GdmError, match="gdm_mass_solve_slab first"):
+            ops[0].mass_solve_interface_rk(xs_copy[0], beta, v0, v0.clone())
+
+
+def test_interface_rk_refusals():
+    """x_local overlapping an output, a partial overlap of acc_out and
+    acc_in, and a single-rank operator are refused."""
+    import gdm_amd
+
+    n, R = (12, 10, 130), 2
+    op = gdm_amd.GdmOperator(3, 5, n, 0.0, 1.0, "mass", n_ranks=R, rank=1)
+    x = op.new_vector(True)
+    op.mass_solve_slab(torch.ones(op.n_owned, dtype=torch.float64, device="cuda"), op.owned_view(x))
+    acc = op.new_vector(True)
+    with pytest.raises(gdm_amd.GdmError, match="must not overlap"):
+        op.mass_solve_interface_rk(x, 1.0, acc, x)
+    big = torch.zeros(op.n_local + 8, dtype=torch.float64, device="cuda")
+    with pytest.raises(gdm_amd.GdmError, match="must not overlap"):
+        op.mass_solve_interface_rk(x, 1.0, big[:op.n_local], big[8:])
+    single = gdm_amd.GdmOperator(3, 5, n, 0.0, 1.0, "mass")
+    v = single.new_vector(True)
+    with pytest.raises(gdm_amd.GdmError, match="multi-rank only"):
+        single.mass_solve_interface_rk(v, 1.0, v.clone(), v.clone())
+
+
 @pytest.mark.parametrize("dim,p,n,R,kind", [(3, 5, (70, 40, 130), 3, "advection"), (2, 5, (90, 150), 4, "advection"),
                                             (3, 7, (40, 33, 255), 8, "advection")])
 def test_one_exchange_rk_step_matches_two_exchange(dim, p, n, R, kind):
@@ -186,13 +272,21 @@ def test_one_exchange_rk_step_matches_two_exchange(dim, p, n, R, kind):
     del pr, one
     ops = [gdm_amd.GdmOperator(dim, p, n, 0.0, 1.0, kind, params=a, rank=r, n_ranks=R) for r in range(R)]
     ps = ops[0].layout["plane_size"]
-    res = {}
-    for one_ex in (False, True):
-        rk = SlabRK4(ops, lambda vs: (torch.cuda.synchronize(), _exchange(ops, vs)), 2, sine, one_exchange=one_ex)
+    res, local = {}, {}
+    for one_ex, fused in ((False, False), (True, False), (True, True)):
+        rk = SlabRK4(ops, lambda vs: (torch.cuda.synchronize(), _exchange(ops, vs)), 2, sine, one_exchange=one_ex,
+                     fused=fused)
         rk.set_solution([u0[op.layout["owned_plane_begin"] * ps:op.layout["owned_plane_end"] * ps] for op in ops])
         for s in range(steps):
             rk.step(s * h, h)
         torch.cuda.synchronize()
-        res[one_ex] = torch.cat([op.owned_view(y) for op, y in zip(ops, rk.y)])
+        res[one_ex, fused] = torch.cat([op.owned_view(y) for op, y in zip(ops, rk.y)])
+        local[one_ex, fused] = [y.clone() for y in rk.y]
+    # the fused interface + update launch (gdm_mass_solve_interface_rk) gives
+    # the bits of interface_ghosts + rk_update, ghost planes included
+    for a_, b_ in zip(local[True, True], local[True, False]):
+        assert torch.equal(a_, b_)
+    res[True] = res[True, True]
+    res[False] = res[False, False]
     assert float(torch.linalg.norm(res[True] - res[False]) / torch.linalg.norm(res[False])) < 1e-13
     assert float(torch.linalg.norm(res[False] - single) / torch.linalg.norm(single)) < 1e-12

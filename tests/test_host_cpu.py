@@ -439,6 +439,10 @@ class _NpSlabRkOp(_NpSpikeOp):
             a[gb + n:gb + n + p] = t
         return x_local
 
+    def mass_solve_interface_rk(self, x_local, beta, acc_in, acc_out, alpha=0.0, y=None, Y=None):
+        k = self.mass_solve_interface_ghosts(x_local.clone())
+        return self.rk_update(beta, k, acc_in, acc_out, alpha, y, Y)
+
 
 def _rk_worker(rank, world, port, p, n, a, steps, q):
     import torch
