@@ -1140,10 +1140,12 @@ bool mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
   const int64_t X = K[0], Y = K[1], Z = K[2];
   // v3 (gdm_mass.hip, single sweep per direction) where supported, else v2
   // (two sweeps).  Large meshes: the first pass reads rhs and writes x, later
-  // passes in place.  A pass with fewer than 512 waves of lines (2D C2: 16)
-  // splits its lines into segments, which read their neighbours' input:
-  // then every pass runs out of place through the scratch vector (ping-pong
-  // ending in x)
+  // passes in place.  A pass with fewer than gdmk_mass3_seg_waves() waves of
+  // lines (2D C2: 16; the y and x passes of a C3 / C4 rank's slab) splits its
+  // lines into segments, which read their neighbours' input: such a pass runs
+  // out of place (x <-> the scratch vector), the others in place, the outputs
+  // chosen from the last pass (x) backwards so that no copy is needed unless
+  // the first pass is segmented and rhs is x
   const bool v3 = gdmk_mass3_chunk(op->p) > 0;
   struct Pass {
     int ax, dir_kind;
@@ -1172,9 +1174,13 @@ bool mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
     const bool span_ok = q.dir_kind != 1 || ((q.len - 1) * q.stride + lanes) * 8 < (int64_t)0x7fffffff;
     return v3 && t.l3 && span_ok && (q.dir_kind == 1 || (q.len % 2 == 0 && aligned));
   };
-  bool segmented = false;
-  for (const Pass &q : passes)
-    segmented = segmented || (v3 && tab[q.ax].l3 && (q.n_lines + 63) / 64 < gdmk_mass3_seg_waves());
+  const int np = (int)passes.size();
+  bool seg[3] = {false, false, false}, segmented = false;
+  for (int i = 0; i < np; ++i) {
+    const Pass &q = passes[(size_t)i];
+    seg[i] = v3 && tab[q.ax].l3 && (q.n_lines + 63) / 64 < gdmk_mass3_seg_waves();
+    segmented = segmented || seg[i];
+  }
   double *tmp = nullptr;
   if (segmented) {
     if (op->mass_tmp_size < n) {  // once per operator (n is the owned size), freed with it
@@ -1184,18 +1190,18 @@ bool mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
     }
     tmp = op->mass_tmp;
   }
+  // pass outputs, last to first: a segmented pass reads the other buffer than
+  // it writes, an unsegmented one may run in place
+  double *outs[3] = {x_owned, x_owned, x_owned};
+  for (int i = np - 1; i > 0; --i) outs[i - 1] = seg[i] ? (outs[i] == x_owned ? tmp : x_owned) : outs[i];
   const double *in = rhs_owned;
-  const int np = (int)passes.size();
   for (int i = 0; i < np; ++i) {
     const Pass &q = passes[(size_t)i];
-    double *out = x_owned;
-    if (segmented) {
-      out = (np - 1 - i) % 2 == 0 ? x_owned : tmp;
-      if (out == in) {  // rhs aliases the first pass's output: move it aside
-        double *other = out == x_owned ? tmp : x_owned;
-        hip_check(hipMemcpyAsync(other, in, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
-        in = other;
-      }
+    double *out = outs[i];
+    if (seg[i] && out == in) {  // rhs aliases the first pass's output: move it aside
+      double *other = out == x_owned ? tmp : x_owned;
+      hip_check(hipMemcpyAsync(other, in, sizeof(double) * n, hipMemcpyDeviceToDevice, op->stream), "copy");
+      in = other;
     }
     const LineTables &t = tab[q.ax];
     if (rk && i == np - 1 && !segmented && !part && q.dir_kind == 0 && use_v3(q, in, in)) {
@@ -1206,7 +1212,7 @@ bool mass_solve_passes(gdm_op *op, const double *rhs_owned, double *x_owned, con
     }
     if (use_v3(q, in, out))
       hip_check(gdmk_launch_mass3(op->p, q.dir_kind, in, out, (int)q.len, q.stride, q.n_lines, q.A, q.B, t.l3, t.u3,
-                                  t.d3, t.cst.data(), t.row_lo, t.row_hi, segmented ? 1 : 0, op->stream),
+                                  t.d3, t.cst.data(), t.row_lo, t.row_hi, seg[i] ? 1 : 0, op->stream),
                 q.what);
     else
       hip_check(gdmk_launch_mass_lines(op->p, q.dir_kind, in, out, (int)q.len, q.stride, q.n_lines, q.A, q.B, t.lrow,
@@ -1668,7 +1674,7 @@ int gdm_mass_solve_interface_rk(gdm_op *op, const double *x_local, double beta, 
                                 double alpha, const double *y, double *Y) {
   if (!op) return fail(GDM_ERR_ARG, "op is NULL");
   if (op->mesh.n_ranks == 1)
-    return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_interface_rk: multi-rank only (one rank: gdm_mass_apply_inverse_rk)");
+    return fail(GDM_ERR_UNSUPPORTED, "gdm_mass_solve_interface_rk: multi-rank only (one rank: gdm_mass_solve_rk)");
   if (!op->spike.built || op->spike.rounds < 0 || op->spike.next_round < 0)
     return fail(GDM_ERR_STATE, "gdm_mass_solve_interface_rk: call gdm_mass_solve_slab first");
   if (op->spike.next_round != op->spike.rounds)

@@ -141,9 +141,9 @@ hipError_t gdmk_launch_mass_lines(int p, int dir_kind, const double *src, double
 int gdmk_mass3_chunk(int p);
 // passes with fewer waves of lines than this run segmented (gdm_mass.hip)
 int gdmk_mass3_seg_waves();
-// allow_segments (src != dst only): lines of a pass with fewer than 512
-// waves are split into segments of >= 1 chunk with warm-ups (one more grid
-// dimension), so small meshes fill the GPU
+// allow_segments (src != dst only): lines of a pass with fewer than
+// gdmk_mass3_seg_waves() waves are split into segments of >= 1 chunk with
+// warm-ups (one more grid dimension), so small meshes fill the GPU
 hipError_t gdmk_launch_mass3(int p, int dir_kind, const double *src, double *dst, int len, int64_t stride,
                              int64_t n_lines, int64_t A, int64_t B, const double *lrow, const double *urow,
                              const double *invd, const double *cst, int row_lo, int row_hi, int allow_segments,

@@ -286,102 +286,107 @@ __global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps,
 }
 
 // The interface correction fused with the RK stage update of the one-exchange
-// stage (gdm_mass_solve_interface_rk): per line, b / t as spike_kernel mode 2,
-// then for every plane of the local layout the stage derivative k -- b / t on
-// the ghost planes below / above, g_k - V[k] t - W[k] b on the owned ones
-// (g_k from G0 on the edge planes after refinement rounds) -- goes straight
-// into acc_out = acc_in + beta k and Y = y + alpha k (local vectors, one FMA
-// each as in rk_update2_kernel); k itself is not stored.  Planes in blocks of
-// KB: one memory latency per block.
+// stage (gdm_mass_solve_interface_rk): for every plane of the local layout the
+// stage derivative k -- b / t (spike_kernel mode 2) on the ghost planes below /
+// above, g_k - V[k] t - W[k] b on the owned ones (g_k from G0 on the edge
+// planes after refinement rounds) -- goes straight into acc_out = acc_in +
+// beta k and Y = y + alpha k (local vectors, one FMA each as in
+// rk_update2_kernel); k itself is not stored.  Grid: (line block, chunk of
+// SRK_CH planes), the chunk index fastest so a line block's chunks run
+// together and their re-reads of the 2 x 2p edge planes behind b / t come
+// from cache; a chunk computes b / t only when it needs them.  Planes in
+// blocks of KB: one memory latency per block.
+constexpr int SRK_CH = 16;
 template <int P, bool WITH_Y>
-__global__ void __launch_bounds__(256) spike_rk_kernel(const double *x_local, int64_t ps, int gb, int ga, int n,
-                                                       int has_lo, int has_hi, const double *__restrict__ VW,
+__global__ void __launch_bounds__(256) spike_rk_kernel(const double *__restrict__ x_local, int64_t ps, int gb, int ga,
+                                                       int n, int has_lo, int has_hi, const double *__restrict__ VW,
                                                        const double *__restrict__ S, int k_begin, int k_end,
-                                                       const double *__restrict__ G0, const RkOut rk) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ps; i += (int64_t)gridDim.x * blockDim.x) {
-    const double *xo = x_local + (int64_t)gb * ps + i;
-    double b[P], t[P], in[2 * P];
+                                                       const double *__restrict__ G0, const RkOut rk, int nch) {
+  const int chunk = (int)(blockIdx.x % (unsigned)nch);
+  const int64_t i = (int64_t)(blockIdx.x / (unsigned)nch) * blockDim.x + threadIdx.x;
+  if (i >= ps) return;
+  const int kb = -gb + chunk * SRK_CH, ke = min(n + ga, kb + SRK_CH);  // planes relative to the first owned one
+  const bool corr = kb < k_end && k_begin < ke;
+  const double *xo = x_local + (int64_t)gb * ps + i;
+  double b[P], t[P], in[2 * P];
 #pragma unroll
-    for (int j = 0; j < P; ++j) b[j] = t[j] = 0.0;
-    if (has_lo) {
+  for (int j = 0; j < P; ++j) b[j] = t[j] = 0.0;
+  if (has_lo && (kb < 0 || corr)) {
 #pragma unroll
-      for (int a = 0; a < P; ++a) {
-        in[a] = xo[(int64_t)(a - P) * ps];
-        in[P + a] = xo[(int64_t)a * ps];
-      }
-#pragma unroll
-      for (int j = 0; j < P; ++j) {
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < 2 * P; ++c) s = fma(S[j * 2 * P + c], in[c], s);
-        b[j] = s;
-      }
+    for (int a = 0; a < P; ++a) {
+      in[a] = xo[(int64_t)(a - P) * ps];
+      in[P + a] = xo[(int64_t)a * ps];
     }
-    if (has_hi) {
 #pragma unroll
-      for (int a = 0; a < P; ++a) {
-        in[a] = xo[(int64_t)(n - P + a) * ps];
-        in[P + a] = xo[(int64_t)(n + a) * ps];
-      }
+    for (int j = 0; j < P; ++j) {
+      double s = 0.0;
 #pragma unroll
-      for (int j = 0; j < P; ++j) {
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < 2 * P; ++c) s = fma(S[2 * P * P + j * 2 * P + c], in[c], s);
-        t[j] = s;
-      }
+      for (int c = 0; c < 2 * P; ++c) s = fma(S[j * 2 * P + c], in[c], s);
+      b[j] = s;
     }
-    using d1 = double;
-    const int kb = -gb, ke = n + ga;  // local planes relative to the first owned one
-    constexpr int KB = 8;
-    for (int k0 = kb; k0 < ke; k0 += KB) {
-      d1 kv[KB], av[KB], yv[KB];
+  }
+  if (has_hi && (ke > n || corr)) {
 #pragma unroll
-      for (int u = 0; u < KB; ++u) {
-        const int k = k0 + u;
-        if (k < ke) {
-          const int64_t e = (int64_t)(gb + k) * ps + i;
-          av[u] = rk.acc_in[e];
-          if (WITH_Y) yv[u] = rk.y[e];
-          if ((k < 0 && !has_lo) || (k >= n && !has_hi)) {
-            kv[u] = xo[(int64_t)k * ps];  // a ghost plane the interface leaves alone
-          } else if (k >= 0 && k < n) {
-            if (G0 && k < P)
-              kv[u] = G0[(int64_t)k * ps + i];
-            else if (G0 && k >= n - P)
-              kv[u] = G0[(int64_t)(P + k - (n - P)) * ps + i];
-            else
-              kv[u] = xo[(int64_t)k * ps];
-          }
+    for (int a = 0; a < P; ++a) {
+      in[a] = xo[(int64_t)(n - P + a) * ps];
+      in[P + a] = xo[(int64_t)(n + a) * ps];
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < 2 * P; ++c) s = fma(S[2 * P * P + j * 2 * P + c], in[c], s);
+      t[j] = s;
+    }
+  }
+  constexpr int KB = 8;
+  for (int k0 = kb; k0 < ke; k0 += KB) {
+    double kv[KB], av[KB], yv[KB];
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const int k = k0 + u;
+      if (k < ke) {
+        const int64_t e = (int64_t)(gb + k) * ps + i;
+        av[u] = __builtin_nontemporal_load(rk.acc_in + e);
+        if (WITH_Y) yv[u] = __builtin_nontemporal_load(rk.y + e);
+        if ((k < 0 && !has_lo) || (k >= n && !has_hi)) {
+          kv[u] = xo[(int64_t)k * ps];  // a ghost plane the interface leaves alone
+        } else if (k >= 0 && k < n) {
+          if (G0 && k < P)
+            kv[u] = G0[(int64_t)k * ps + i];
+          else if (G0 && k >= n - P)
+            kv[u] = G0[(int64_t)(P + k - (n - P)) * ps + i];
+          else
+            kv[u] = xo[(int64_t)k * ps];
         }
       }
+    }
 #pragma unroll
-      for (int u = 0; u < KB; ++u) {
-        const int k = k0 + u;
-        if (k < ke) {
-          double kval;
-          if (k < 0 && has_lo) {
-            kval = b[k + P];
-          } else if (k >= n && has_hi) {
-            kval = t[k - n];
-          } else if (k < 0 || k >= n) {
-            kval = kv[u];
-          } else {
-            kval = kv[u];
-            if (k >= k_begin && k < k_end) {
-              const double *vw = VW + (size_t)k * 2 * P;
-              double c = 0.0;
+    for (int u = 0; u < KB; ++u) {
+      const int k = k0 + u;
+      if (k < ke) {
+        double kval;
+        if (k < 0 && has_lo) {
+          kval = b[k + P];
+        } else if (k >= n && has_hi) {
+          kval = t[k - n];
+        } else if (k < 0 || k >= n) {
+          kval = kv[u];
+        } else {
+          kval = kv[u];
+          if (k >= k_begin && k < k_end) {
+            const double *vw = VW + (size_t)k * 2 * P;
+            double c = 0.0;
 #pragma unroll
-              for (int j = 0; j < P; ++j) c = fma(vw[j], t[j], c);
+            for (int j = 0; j < P; ++j) c = fma(vw[j], t[j], c);
 #pragma unroll
-              for (int j = 0; j < P; ++j) c = fma(vw[P + j], b[j], c);
-              kval = kval - c;
-            }
+            for (int j = 0; j < P; ++j) c = fma(vw[P + j], b[j], c);
+            kval = kval - c;
           }
-          const int64_t e = (int64_t)(gb + k) * ps + i;
-          if (WITH_Y) rk.Y[e] = fma(rk.alpha, kval, yv[u]);
-          rk.acc_out[e] = fma(rk.beta, kval, av[u]);
         }
+        const int64_t e = (int64_t)(gb + k) * ps + i;
+        if (WITH_Y) __builtin_nontemporal_store(fma(rk.alpha, kval, yv[u]), rk.Y + e);
+        __builtin_nontemporal_store(fma(rk.beta, kval, av[u]), rk.acc_out + e);
       }
     }
   }
@@ -392,16 +397,19 @@ __global__ void __launch_bounds__(256) spike_rk_kernel(const double *x_local, in
 extern "C" hipError_t gdmk_launch_spike_rk(int p, const double *x_local, int64_t ps, int gb, int ga, int n,
                                           int has_lo, int has_hi, const double *VW, const double *S, int k_begin,
                                           int k_end, const double *G0, const gdmk::RkOut &rk, hipStream_t st) {
-  if (ps <= 0) return hipSuccess;
-  const unsigned blocks = (unsigned)std::min<int64_t>((ps + 255) / 256, 4096);
+  if (ps <= 0 || n + gb + ga <= 0) return hipSuccess;
+  const int nch = (n + gb + ga + gdmk::SRK_CH - 1) / gdmk::SRK_CH;
+  const int64_t nb = ((ps + 255) / 256) * nch;
+  if (nb > 0x7fffffff) return hipErrorInvalidValue;
+  const unsigned blocks = (unsigned)nb;
 #define GDM_SPIKE_RK(PP)                                                                                        \
   case PP:                                                                                                      \
     if (rk.Y)                                                                                                   \
       hipLaunchKernelGGL((gdmk::spike_rk_kernel<PP, true>), dim3(blocks), dim3(256), 0, st, x_local, ps, gb, ga, \
-                         n, has_lo, has_hi, VW, S, k_begin, k_end, G0, rk);                                     \
+                         n, has_lo, has_hi, VW, S, k_begin, k_end, G0, rk, nch);                                \
     else                                                                                                        \
       hipLaunchKernelGGL((gdmk::spike_rk_kernel<PP, false>), dim3(blocks), dim3(256), 0, st, x_local, ps, gb,   \
-                         ga, n, has_lo, has_hi, VW, S, k_begin, k_end, G0, rk);                                 \
+                         ga, n, has_lo, has_hi, VW, S, k_begin, k_end, G0, rk, nch);                            \
     break;
   switch (p) {
     GDM_SPIKE_RK(1)
