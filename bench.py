@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--rank-timeout", type=float, default=1800.0,
                     help="--gpus N without a launcher: seconds before hung rank processes are terminated")
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="before the W warm-up steps: untimed steps until this much wall time has passed (the "
+                         "clock ramp of a fresh GPU: the first ~25 back-to-back launches run 5-40 %% slower, "
+                         "profiles/r6k); reported as settle_steps; 0 = off")
     ap.add_argument("--n", type=int, default=511, help="cells per direction per GPU slab (vertices = n + 1)")
     ap.add_argument("--p", type=int, default=5)
     ap.add_argument("--kind", default="advection", choices=["advection", "wave", "mass"])
@@ -652,6 +656,24 @@ def main():
         if ev is not None:
             ev[1].record(stream)
 
+    # settle: the GPU's clocks ramp over the first ~25 back-to-back launches of a fresh process
+    # (profiles/r6k/README.md); untimed, before and in addition to the W warm-up steps
+    settle_steps = 0
+    if args.settle_ms > 0:
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        while True:
+            for _ in range(10):
+                step()
+            settle_steps += 10
+            torch.cuda.synchronize()
+            done = (time.perf_counter() - ts) * 1e3 >= args.settle_ms or settle_steps >= 100000
+            if dist is not None:  # every rank runs the same steps (the halo exchanges pair up)
+                f = torch.tensor([1.0 if done else 0.0], device="cuda")
+                dist.all_reduce(f, op=dist.ReduceOp.MAX)
+                done = float(f) > 0.0
+            if done:
+                break
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -728,6 +750,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle_steps": settle_steps,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "weak" if (weak and world > 1) else "strong",
