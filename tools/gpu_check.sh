@@ -20,4 +20,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ks" -o ks --output-f
   python -u bench.py --metric-only > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err"; rc=$?
 echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 find "$OUT/ks" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
+find "$OUT/ks" -name "*kernel_trace.csv" -exec cp {} "$OUT/kernel_trace.csv" \;
+# the stats average every launch (settle + warm-up + timed); the timed steps alone:
+python3 tools/trace_avg.py "$OUT/kernel_trace.csv" 50 > "$OUT/kernel_timed_avg.txt"
 exit 0
