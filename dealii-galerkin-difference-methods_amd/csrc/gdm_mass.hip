@@ -657,13 +657,22 @@ __global__ void __launch_bounds__(64) mass3_rows_kernel(const double *src, doubl
   // the lane index passes through an opaque VGPR move in the helpers below:
   // otherwise LICM keeps every per-instruction (row, pair) offset of the DMA
   // and the stores live across the march loop (~100 VGPRs)
+  // The LDS row's pad pair (pair UPR - 1, positions base + C, base + C + 1) is
+  // never read back, and positions past the line end (the last chunk) only
+  // meet zero table coefficients: those lanes take an offset past the
+  // resource's range (the load returns zeros without a memory request).
+  // Fetching the pad pulled a 4th 128-B line into every 384-B chunk row: 1.31x
+  // the x pass's algorithmic reads, 1.03x after it, 1.00x with the line end
+  // (FETCH_SIZE, profiles/r6p)
   auto dma = [&](ldouble2 *t, int base) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int q = 0; q < UPR; ++q) {
       const int u = q * 64 + ln, row = u / UPR, pair = u - row * UPR;
-      const uint32_t voff = (uint32_t)(((int64_t)row * len + base + 2 * pair) * 8);
+      const uint32_t voff = (pair == UPR - 1 || base + 2 * pair >= len)
+                                ? 0x7ffffff0u
+                                : (uint32_t)(((int64_t)row * len + base + 2 * pair) * 8);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(t + q * 64), 16,
                                                voff, 0, 0, GDM_MASS_LD_CPOL);
     }
