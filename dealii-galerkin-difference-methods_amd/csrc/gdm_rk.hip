@@ -292,18 +292,24 @@ __global__ void __launch_bounds__(256) spike_kernel(double *x_local, int64_t ps,
 // planes after refinement rounds) -- goes straight into acc_out = acc_in +
 // beta k and Y = y + alpha k (local vectors, one FMA each as in
 // rk_update2_kernel); k itself is not stored.  Grid: (line block, chunk of
-// SRK_CH planes), the chunk index fastest so a line block's chunks run
-// together and their re-reads of the 2 x 2p edge planes behind b / t come
-// from cache; a chunk computes b / t only when it needs them.  Planes in
-// blocks of KB: one memory latency per block.
+// SRK_CH planes), laid out so that the chunks of a line block are 8 block ids
+// apart: consecutive ids go to the 8 XCDs in turn, so all chunks of a line
+// block run on one XCD, close in time, and their re-reads of the 2 x 2p edge
+// planes behind b / t hit that XCD's L2 (chunk-fastest ids spread them over
+// all eight L2s: 1.4x the kernel's algorithmic fetch, profiles/r6r).  A chunk
+// computes b / t only when it needs them.  Planes in blocks of KB: one memory
+// latency per block.
 constexpr int SRK_CH = 16;
 template <int P, bool WITH_Y>
 __global__ void __launch_bounds__(256) spike_rk_kernel(const double *__restrict__ x_local, int64_t ps, int gb, int ga,
                                                        int n, int has_lo, int has_hi, const double *__restrict__ VW,
                                                        const double *__restrict__ S, int k_begin, int k_end,
                                                        const double *__restrict__ G0, const RkOut rk, int nch) {
-  const int chunk = (int)(blockIdx.x % (unsigned)nch);
-  const int64_t i = (int64_t)(blockIdx.x / (unsigned)nch) * blockDim.x + threadIdx.x;
+  // block id = (lb / 8) * 8 nch + chunk * 8 + lb % 8
+  const unsigned bid = blockIdx.x, g = bid / (8u * (unsigned)nch), rem = bid - g * 8u * (unsigned)nch;
+  const int chunk = (int)(rem / 8u);
+  const int64_t lb = (int64_t)g * 8 + (rem % 8u);
+  const int64_t i = lb * blockDim.x + threadIdx.x;
   if (i >= ps) return;
   const int kb = -gb + chunk * SRK_CH, ke = min(n + ga, kb + SRK_CH);  // planes relative to the first owned one
   const bool corr = kb < k_end && k_begin < ke;
@@ -399,7 +405,7 @@ extern "C" hipError_t gdmk_launch_spike_rk(int p, const double *x_local, int64_t
                                           int k_end, const double *G0, const gdmk::RkOut &rk, hipStream_t st) {
   if (ps <= 0 || n + gb + ga <= 0) return hipSuccess;
   const int nch = (n + gb + ga + gdmk::SRK_CH - 1) / gdmk::SRK_CH;
-  const int64_t nb = ((ps + 255) / 256) * nch;
+  const int64_t nb = ((ps + 255) / 256 + 7) / 8 * 8 * nch;  // line blocks padded to a multiple of 8
   if (nb > 0x7fffffff) return hipErrorInvalidValue;
   const unsigned blocks = (unsigned)nb;
 #define GDM_SPIKE_RK(PP)                                                                                        \
